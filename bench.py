@@ -1,0 +1,291 @@
+"""Benchmark: NNGP Gram-matrix build (kernel entries/s) + GP solve on MI355X.
+
+Workload (BASELINE.json configs[1]): mnist_paper_convnet_gp, Kxx of N = 4096 synthetic
+28×28×1 images, float64, Gram tiles of B = 1024 (the reference's tile schedule:
+upper-triangular tiles, diagonal tiles evaluated in full).  One STEP = every Gram tile of
+this rank evaluated into a device-resident Kxx.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config C --n N --tile B]
+
+Multi-GPU (one process per GPU, torchrun): the Gram tiles of a Kxx whose size grows with
+the world (n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world) are split across ranks with
+the reference's contiguous balanced split (cnn_gp/data.py:11-19) — no data-path
+collective; per-rank work is ~constant ("scaling": "weak").
+
+value = evaluated pairs (Σ over all tiles of B1·B2) per second, whole job.  Also
+reported: unique Kxx entries/s, the single-GPU build+solve wall-clock (rocSOLVER
+dpotrf+dpotrs on the assembled Kxx, NaN lower triangle), the dominant kernel's HBM
+roofline fraction measured live with HIP events, and the CPU oracle's rate on a bounded
+sample of the same workload (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import cnn_gp  # noqa: E402
+from cnn_gp import _native as N  # noqa: E402
+from cnn_gp.data import tile_schedule  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="mnist_paper_convnet_gp")
+    p.add_argument("--n", type=int, default=4096, help="Kxx size at world size 1")
+    p.add_argument("--tile", type=int, default=1024)
+    p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    p.add_argument("--no-solve", action="store_true")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-probe", action="store_true")
+    p.add_argument("--cpu-pairs", type=int, default=4096,
+                   help="pairs in the CPU-oracle sample (64x64 tile = 4096)")
+    return p.parse_args()
+
+
+def blocks_for_world(n1: int, tile: int, world: int) -> int:
+    """Smallest n_blocks whose upper-triangular tile count covers world × the 1-GPU one."""
+    b1 = -(-n1 // tile)
+    target = b1 * (b1 + 1) // 2 * world
+    nb = b1
+    while nb * (nb + 1) // 2 < target:
+        nb += 1
+    return nb
+
+
+def op_bytes(op, nmaps, n1, n2, C, item):
+    """Algorithmic HBM bytes of one pair-pipeline launch."""
+    h, w = op.shape_in
+    ho, wo = op.shape_out
+    if op.kind == "conv":
+        rd = (n1 + n2) * C * h * w if op.pre == N.CGP_PRE_MOMENTS else nmaps * h * w
+        b = rd + nmaps * ho * wo
+        if op.addend is not None:
+            b += nmaps * ho * wo
+        if op.pre == N.CGP_PRE_RELU:
+            b += (n1 + n2) * h * w
+        if op.post == N.CGP_POST_RELU:
+            b += (n1 + n2) * ho * wo
+    elif op.kind == "relu":
+        b = 2 * nmaps * ho * wo + (n1 + n2) * ho * wo + (nmaps * ho * wo if op.addend else 0)
+    else:
+        b = (2 * len(op.terms)) * nmaps * ho * wo
+    return b * item
+
+
+def op_name(op):
+    if op.kind == "conv":
+        pre = {0: "", 1: "relu+", 2: "moments+"}[op.pre]
+        post = "+relu" if op.post else ""
+        add = "+add" if op.addend is not None else ""
+        return (f"{pre}conv{op.geom.taps}s{op.geom.stride}{post}{add}"
+                f"@{op.shape_in[0]}->{op.shape_out[0]}")
+    return f"{op.kind}@{op.shape_out[0]}"
+
+
+def probe_kernels(model, x, n1, n2, reps=10):
+    """Time every launch of one full tile's pair program with HIP events on the stream the
+    kernels run on; return per-op (name, avg_ms, alg_bytes)."""
+    from cnn_gp.program import Plan
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    _, C, h, w = x.shape
+    plan = model._plan(h, w)
+    sfx = Plan._sfx(x.dtype)
+    lib = N.load()
+    var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
+    N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(x), n1, n2, C, h * w,
+                                                    N.ptr(var0[:n1]), N.ptr(var0[n1:]), s), "mv")
+    var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, False, s)
+    xy0 = None
+    if not plan.moments_fused:
+        xy0 = torch.empty((n1 * n2, h, w), dtype=x.dtype, device=x.device)
+        N.check(getattr(lib, f"cgp_moments_xy_{sfx}")(N.ptr(x), N.ptr(x), n1, n2, C, h * w, 0,
+                                                       N.ptr(xy0), s), "mxy")
+    res = []
+    item = x.element_size()
+
+    def probe(idx, op, launch):
+        launch()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        res.append((op_name(op), ms, op_bytes(op, n1 * n2, n1, n2, C, item)))
+
+    plan.run_pairs(x, x, xy0, var, n1, n2, False, False, s, probe=probe)
+    torch.cuda.synchronize()
+    return res
+
+
+def cpu_baseline(cfg_name, dtype, pairs):
+    """The CPU oracle (numpy restatement, 1 thread) on a bounded sample: one Kxz tile."""
+    from oracle import nngp_oracle as O
+    from oracle import specs
+    side = int(round(pairs ** 0.5))
+    spec = specs.CONFIGS[cfg_name]()
+    C, hw = specs.GEOMETRY[cfg_name]
+    rng = np.random.default_rng(0)
+    dt = np.float64 if dtype == torch.float64 else np.float32
+    X = rng.random((side, C, hw, hw)).astype(dt)
+    Z = rng.random((side, C, hw, hw)).astype(dt)
+    t0 = time.perf_counter()
+    O.kernel(spec, X, Z, False, False)
+    el = time.perf_counter() - t0
+    return dict(value=round(side * side / el, 1), unit="pairs/s", cores=1, kind="port",
+                sample=f"one {side}x{side} Kxz tile of {cfg_name} ({side*side} pairs, "
+                       f"{'f64' if dt == np.float64 else 'f32'}) through oracle/nngp_oracle.py "
+                       f"in {el:.1f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dtype = torch.float64 if args.dtype == "f64" else torch.float32
+
+    cfg = importlib.import_module(f"configs.{args.config}")
+    model = cfg.initial_model.to(dev, dtype)
+    C = getattr(cfg, "in_channels", 1)
+    side = 32 if C == 3 else 28
+    B = args.tile
+    nb = blocks_for_world(args.n, B, world)
+    n_total = nb * B if world > 1 else args.n
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = torch.rand((n_total, C, side, side), generator=g, dtype=dtype).to(dev)
+
+    tiles = tile_schedule(n_total, None, B, rank, world)
+    all_tiles = tile_schedule(n_total, None, B, 0, 1)
+
+    def tile_pairs(t):
+        _, i, j = t
+        return (min(B, n_total - i * B)) * (min(B, n_total - j * B))
+
+    pairs_total = sum(tile_pairs(t) for t in all_tiles)
+    K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
+
+    def step():
+        with torch.no_grad():
+            for same, i, j in tiles:
+                xi = X[i * B:(i + 1) * B]
+                if same:
+                    k = model(xi)
+                else:
+                    k = model(xi, X[j * B:(j + 1) * B], False, False)
+                K[i * B:i * B + k.shape[0], j * B:j * B + k.shape[1]].copy_(k)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms_step = elapsed / args.steps * 1e3
+    value = pairs_total * args.steps / elapsed
+
+    extra = {}
+    # --- solve of the assembled Kxx (single GPU) ---
+    if rank == 0 and world == 1 and not args.no_solve:
+        labels = torch.randint(0, 10, (n_total,), generator=g)
+        Y = cnn_gp.one_hot_pm1(labels, 10).to(dev)
+        Kc = K.clone()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        cnn_gp.solve_system(Kc, Y, jitter=1e-6)
+        torch.cuda.synchronize()
+        t_solve = time.perf_counter() - t1
+        extra["solve_s"] = round(t_solve, 4)
+        extra["build_solve_wall_s"] = round(ms_step / 1e3 + t_solve, 4)
+        extra["solve_gflops"] = round(n_total ** 3 / 3 / t_solve / 1e9, 1)
+        del Kc
+
+    # --- dominant kernel, timed live ---
+    roof = None
+    if rank == 0 and not args.no_probe:
+        with torch.no_grad():
+            ops = probe_kernels(model, X[:B], B, B)
+        by = {}
+        for name, ms, b in ops:
+            t = by.setdefault(name, [0.0, 0, 0.0, 0])
+            t[0] += ms
+            t[1] += 1
+            t[2] += b
+            t[3] = b
+        dom = max(by.items(), key=lambda kv: kv[1][0])
+        name, (tot_ms, cnt, _, b_launch) = dom
+        avg_ms = tot_ms / cnt
+        achieved = b_launch / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
+                "alg_bytes_per_launch": int(b_launch)}
+        extra["kernel_breakdown_ms_per_tile"] = {k: round(v[0], 3) for k, v in by.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.config, dtype, args.cpu_pairs)
+
+    if rank == 0:
+        line = {
+            "metric": "kernel entries/s (N×M pairs) + full-Kxx build+solve wall-clock, "
+                      "MNIST 28×28",
+            "value": round(value, 1),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (torch.rand seed 0, 28x28x1)",
+            "config": {"workload": f"{args.config} Kxx {n_total}x{n_total}, tiles {B}",
+                       "n": n_total, "tile": B, "tiles_total": len(all_tiles),
+                       "tiles_rank0": len(tiles), "pairs_per_step": pairs_total,
+                       "parallelism": f"tiles-dp{world}"},
+            "unique_entries_per_s": round(n_total * (n_total + 1) / 2 * args.steps / elapsed, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,221 @@
+"""Tile schedule, worker split and dataset plumbing (reference: cnn_gp/data.py).
+
+The Gram matrix is evaluated in B×B tiles.  ``ProductIterator`` yields the reference's
+tile order — for Kxx the upper triangle row by row, diagonal tile first (data.py:22-29),
+for Kxz every tile — and gives worker ``r`` of ``n`` a contiguous, balanced slice of it
+(data.py:11-19, 54-60).  Multi-GPU Gram assembly (gram.py) uses the same split, so a
+rank's tiles are exactly the reference worker's.
+
+Differences from the reference, all bug fixes that keep the documented behaviour:
+``np.int`` (removed in numpy 1.24, data.py:12) is not used; ``DiagIterator`` with a
+second dataset unpacks ``enumerate(zip(...))`` correctly (data.py:124 raises).
+``DatasetFromConfig`` reads MNIST from local IDX files (no network download).
+"""
+from __future__ import annotations
+
+import gzip
+import itertools
+import os
+import time
+
+import numpy as np
+import torch
+from torch.utils.data import ConcatDataset, DataLoader, Subset, TensorDataset
+
+__all__ = ("DatasetFromConfig", "ProductIterator", "DiagIterator", "print_timings",
+           "tile_schedule", "worker_slice")
+
+
+def worker_slice(n_batches: int, worker_rank: int, n_workers: int):
+    """(start, count) of this worker's contiguous share (data.py:11-19): every worker
+    gets n_batches // n_workers, the first n_batches % n_workers one more."""
+    if not 0 <= worker_rank < n_workers:
+        raise ValueError(f"worker_rank {worker_rank} not in [0, {n_workers})")
+    base, extra = divmod(n_batches, n_workers)
+    start = worker_rank * base + min(worker_rank, extra)
+    return start, base + (1 if worker_rank < extra else 0)
+
+
+def _tile_order(bx: int, bx2: int, same: bool):
+    for i in range(bx):
+        if same:
+            yield True, i, i
+        for j in range(i + 1 if same else 0, bx2):
+            yield False, i, j
+
+
+def _ceil_div(a, b):
+    return -(-a // b)
+
+
+def tile_schedule(n_x: int, n_x2, batch_size: int, worker_rank: int = 0, n_workers: int = 1):
+    """This worker's tiles as (same, i_block, j_block) in the reference's order."""
+    bx = _ceil_div(n_x, batch_size)
+    if n_x2 is None:
+        same, bx2 = True, bx
+        n_batches = max(1, bx * (bx + 1) // 2)
+    else:
+        same, bx2 = False, _ceil_div(n_x2, batch_size)
+        n_batches = bx * bx2
+    start, count = worker_slice(n_batches, worker_rank, n_workers)
+    return list(itertools.islice(_tile_order(bx, bx2, same), start, start + count))
+
+
+class ProductIterator:
+    """Iterates this worker's Gram tiles, yielding
+    ``(same, (i0, x_batch), (j0, x2_batch))`` with the batches as the DataLoader
+    collates them (data.py:36-96)."""
+
+    def __init__(self, batch_size, X, X2=None, worker_rank=0, n_workers=1):
+        self.same = X2 is None
+        self.X = X
+        self.X2 = X if X2 is None else X2
+        self.batch_size = batch_size
+        self.worker_rank = worker_rank
+        self.tiles = tile_schedule(len(X), None if X2 is None else len(X2), batch_size,
+                                   worker_rank, n_workers)
+        self._it = iter(self.tiles)
+        self._cache_i = (None, None)
+
+    def __len__(self):
+        return len(self.tiles)
+
+    def __iter__(self):
+        return self
+
+    def _batch(self, dataset, b):
+        lo = b * self.batch_size
+        sub = Subset(dataset, range(lo, min(lo + self.batch_size, len(dataset))))
+        return next(iter(DataLoader(sub, batch_size=self.batch_size)))
+
+    def __next__(self):
+        same, i, j = next(self._it)
+        if self._cache_i[0] != i:
+            self._cache_i = (i, self._batch(self.X, i))
+        xb = self._cache_i[1]
+        x2b = xb if (self.same and i == j) else self._batch(self.X2, j)
+        return same, (i * self.batch_size, xb), (j * self.batch_size, x2b)
+
+
+class DiagIterator:
+    """Batches for the kernel diagonal (data.py:99-126); never split across workers."""
+
+    def __init__(self, batch_size, X, X2=None):
+        self.batch_size = batch_size
+        dl = DataLoader(X, batch_size=batch_size)
+        if X2 is None:
+            self.same = True
+            self.it = iter(enumerate(dl))
+            self.length = len(dl)
+        else:
+            dl2 = DataLoader(X2, batch_size=batch_size)
+            self.same = False
+            self.it = iter(enumerate(zip(dl, dl2)))
+            self.length = min(len(dl), len(dl2))
+
+    def __iter__(self):
+        return self
+
+    def __len__(self):
+        return self.length
+
+    def __next__(self):
+        if self.same:
+            i, xy = next(self.it)
+            xy2 = xy
+        else:
+            i, (xy, xy2) = next(self.it)
+        ib = i * self.batch_size
+        return self.same, (ib, xy), (ib, xy2)
+
+
+def _hhmmss(s):
+    m, s = divmod(int(s), 60)
+    h, m = divmod(m, 60)
+    return f"{m:02d}:{s:02d}" if h == 0 else f"{h:02d}:{m:02d}:{s:02d}"
+
+
+def print_timings(iterator, desc="time", print_interval=2.):
+    """Progress lines (it/s, elapsed<eta) at most every print_interval s (data.py:174-196)."""
+    start = time.perf_counter()
+    total = len(iterator)
+    last = -print_interval
+    for i, value in enumerate(iterator):
+        yield value
+        elapsed = time.perf_counter() - start
+        rate = (i + 1) / elapsed if elapsed > 0 else float("inf")
+        if elapsed > last + print_interval:
+            eta = total / rate if rate > 0 else 0.0
+            print(f"{desc}: {i + 1}/{total} it, {rate:.02f} it/s,"
+                  f"[{_hhmmss(elapsed)}<{_hhmmss(eta)}]")
+            last = elapsed
+
+
+# ------------------------------------------------------------------------------------
+# datasets (data.py:129-162) — local files only
+# ------------------------------------------------------------------------------------
+_MNIST_FILES = {
+    True: ("train-images-idx3-ubyte", "train-labels-idx1-ubyte"),
+    False: ("t10k-images-idx3-ubyte", "t10k-labels-idx1-ubyte"),
+}
+
+
+def _open_maybe_gz(base):
+    for path, opener in ((base, open), (base + ".gz", gzip.open)):
+        if os.path.exists(path):
+            return opener(path, "rb")
+    raise FileNotFoundError(base + "[.gz]")
+
+
+def read_idx(path_base) -> np.ndarray:
+    """Parse an IDX file (MNIST's format: magic 0x0000 <type> <ndim>, big-endian dims)."""
+    with _open_maybe_gz(path_base) as f:
+        raw = f.read()
+    if len(raw) < 4 or raw[0] != 0 or raw[1] != 0:
+        raise ValueError(f"{path_base}: not an IDX file")
+    dtypes = {0x08: np.uint8, 0x09: np.int8, 0x0B: ">i2", 0x0C: ">i4", 0x0D: ">f4",
+              0x0E: ">f8"}
+    dt = np.dtype(dtypes[raw[2]])
+    ndim = raw[3]
+    dims = [int.from_bytes(raw[4 + 4 * k:8 + 4 * k], "big") for k in range(ndim)]
+    off = 4 + 4 * ndim
+    return np.frombuffer(raw, dtype=dt, count=int(np.prod(dims)), offset=off).reshape(dims)
+
+
+def load_mnist(root: str, train: bool):
+    """MNIST as torchvision's ToTensor() sees it: float32 in [0, 1], [N, 1, 28, 28],
+    plus int64 labels.  Looks in root/, root/raw/ and root/MNIST/raw/."""
+    img_name, lbl_name = _MNIST_FILES[train]
+    for d in (root, os.path.join(root, "raw"), os.path.join(root, "MNIST", "raw")):
+        try:
+            imgs = read_idx(os.path.join(d, img_name))
+            lbls = read_idx(os.path.join(d, lbl_name))
+        except FileNotFoundError:
+            continue
+        x = torch.from_numpy(imgs.astype(np.float32) / 255.0).unsqueeze(1)
+        return TensorDataset(x, torch.from_numpy(lbls.astype(np.int64)))
+    raise FileNotFoundError(
+        f"MNIST IDX files ({img_name}, {lbl_name}) not found under {root} "
+        "(this build never downloads; place the files there)")
+
+
+class DatasetFromConfig:
+    """train/validation/test Subsets of ConcatDataset([train, test]) by the config's
+    ranges (data.py:134-158).  Reads local files; supports dataset_name "MNIST"."""
+
+    def __init__(self, datasets_path, config):
+        self.config = config
+        name = getattr(config, "dataset_name", "MNIST")
+        root = os.path.join(datasets_path, name)
+        if name != "MNIST":
+            raise NotImplementedError(f"dataset {name!r}: only local MNIST IDX is supported")
+        train_full = load_mnist(root, True)
+        test_full = load_mnist(root, False)
+        self.data_full = ConcatDataset([train_full, test_full])
+        self.train = Subset(self.data_full, config.train_range)
+        self.validation = Subset(self.data_full, config.validation_range)
+        self.test = Subset(self.data_full, config.test_range)
+
+    @staticmethod
+    def load_full(dataset):
+        return next(iter(DataLoader(dataset, batch_size=len(dataset))))

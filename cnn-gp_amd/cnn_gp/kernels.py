@@ -1,0 +1,245 @@
+"""Drop-in NNGP kernel modules (reference: cnn_gp/kernels.py), evaluated on MI355X.
+
+Same constructors, attributes and call surface as the reference —
+``Sequential(*mods)(x, y=None, same=None, diag=False)`` — but ``forward`` runs a fused
+device program (program.py) through libcnngp.so instead of torch ops.  Tensors are
+storage only: no torch compute runs on the pair maps.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .program import Plan
+
+__all__ = ("NNGPKernel", "Conv2d", "ReLU", "Sequential", "Mixture", "Sum", "resnet_block")
+
+
+def _stream_handle(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _to_device(t: torch.Tensor, device) -> torch.Tensor:
+    if t.device != device:
+        t = t.to(device, non_blocking=True)
+    return t.contiguous()
+
+
+class NNGPKernel(nn.Module):
+    """Base class; ``forward`` mirrors kernels.py:18-57."""
+
+    def _plan(self, h: int, w: int) -> Plan:
+        cache = self.__dict__.setdefault("_cgp_plans", {})
+        fusion = getattr(self, "_cgp_fusion", True)
+        key = (h, w, fusion, self._structure_key())
+        plan = cache.get(key)
+        if plan is None:
+            plan = Plan(self, h, w, enable_fusion=fusion)
+            cache[key] = plan
+        return plan
+
+    def _structure_key(self):
+        """Changes whenever a hyper-parameter the program depends on changes."""
+        key = []
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                # host-side attributes only: reading the (device) buffer would sync
+                key.append(("c", m.kernel_size, m.stride, m.padding, m.dilation,
+                            float(m.var_weight), float(m.var_bias), m.kernel.dtype))
+            elif isinstance(m, Mixture):
+                key.append(("m", tuple(m.proportions())))
+            else:
+                key.append((type(m).__name__, len(getattr(m, "mods", ()))))
+        return tuple(key)
+
+    def set_fusion(self, enabled: bool):
+        """Enable/disable op fusion in the pair pipeline (for A/B tests; default on)."""
+        for m in self.modules():
+            m.__dict__["_cgp_fusion"] = bool(enabled)
+        return self
+
+    def forward(self, x, y=None, same=None, diag=False):
+        """[N1,C,H,W] × [N2,C,H,W] -> kernel [N1,N2] (or [N1] when diag)."""
+        if y is None:                                            # kernels.py:23-26
+            assert same is None
+            y = x
+            same = True
+        assert not diag or len(x) == len(y), (
+            "diagonal kernels must operate with data of equal length")
+        assert 4 == len(x.size())
+        assert 4 == len(y.size())
+        assert x.size(1) == y.size(1)
+        assert x.size(2) == y.size(2)
+        assert x.size(3) == y.size(3)
+        same = bool(same)
+        diag = bool(diag)
+        if x.dtype not in (torch.float32, torch.float64):
+            raise TypeError(f"cnn_gp kernels compute in float32 or float64, got {x.dtype}")
+        out_device = x.device
+        if x.device.type == "cuda":
+            dev = x.device
+        else:
+            if not torch.cuda.is_available():
+                raise RuntimeError("cnn_gp on MI355X needs a HIP device: no GPU is visible "
+                                   "(there is no CPU path)")
+            dev = torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(dev):
+            xd = _to_device(x, dev)
+            yd = xd if y is x else _to_device(y.to(x.dtype), dev)
+            r = self._run(xd, yd, same, diag, _stream_handle(dev))
+        return r.to(out_device) if out_device != dev else r
+
+    def _run(self, x, y, same, diag, stream):
+        n1, c, h, w = x.shape
+        n2 = y.shape[0]
+        plan = self._plan(h, w)
+        sfx = Plan._sfx(x.dtype)
+        lib = N.load()
+        # per-image variances of the inputs (kernels.py:48-49)
+        var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
+        N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, c, h * w,
+                                                        N.ptr(var0[:n1]), N.ptr(var0[n1:]),
+                                                        stream), "cgp_moments_var")
+        var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, stream)
+        xy0 = None
+        if not plan.moments_fused:
+            nmaps = n1 if diag else n1 * n2
+            xy0 = torch.empty((nmaps, h, w), dtype=x.dtype, device=x.device)
+            N.check(getattr(lib, f"cgp_moments_xy_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, c, h * w,
+                                                           int(diag), N.ptr(xy0), stream),
+                    "cgp_moments_xy")
+        out = plan.run_pairs(x, y, xy0, var, n1, n2, same, diag, stream)
+        if plan.final_hw != (1, 1):                              # kernels.py:53-57
+            raise RuntimeError(f"the model's output is {plan.final_hw[0]}x{plan.final_hw[1]}"
+                               " per pair, not 1x1: add a final Conv2d covering the map")
+        return out.view(n1) if diag else out.view(n1, n2)
+
+    def layers(self):
+        return 0
+
+
+class Conv2d(NNGPKernel):
+    """kernels.py:60-98 — constant k×k kernel of value var_weight/k², plus var_bias."""
+
+    def __init__(self, kernel_size, stride=1, padding="same", dilation=1,
+                 var_weight=1., var_bias=0., in_channel_multiplier=1,
+                 out_channel_multiplier=1):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.stride = stride
+        self.dilation = dilation
+        self.var_weight = var_weight
+        self.var_bias = var_bias
+        self.kernel_has_row_of_zeros = False
+        self._padding_arg = padding
+        if padding == "same":
+            self.padding = dilation * (kernel_size // 2)
+            self.kernel_has_row_of_zeros = kernel_size % 2 == 0
+        else:
+            self.padding = padding
+        # the reference's kernel buffer: default dtype (float32), so model.double()
+        # yields float32-rounded weights — kept for identical numerics and for
+        # .cuda()/.double() semantics
+        side = kernel_size + 1 if self.kernel_has_row_of_zeros else kernel_size
+        kernel = torch.ones(1, 1, side, side)
+        if self.kernel_has_row_of_zeros:
+            kernel[:, :, 0, :] = 0.
+            kernel[:, :, :, 0] = 0.
+        self.register_buffer("kernel", kernel * (self.var_weight / self.kernel_size ** 2))
+        self.in_channel_multiplier = in_channel_multiplier
+        self.out_channel_multiplier = out_channel_multiplier
+
+    def layers(self):
+        return 1
+
+    def extra_repr(self):
+        return (f"kernel_size={self.kernel_size}, stride={self.stride}, "
+                f"padding={self.padding}, dilation={self.dilation}, "
+                f"var_weight={self.var_weight}, var_bias={self.var_bias}")
+
+
+class ReLU(NNGPKernel):
+    """kernels.py:128-165 — the arc-cosine covariance map (device: relu_cov)."""
+    f32_tiny = np.finfo(np.float32).tiny
+
+    def layers(self):
+        return 0
+
+
+class Sequential(NNGPKernel):
+    """kernels.py:178-200."""
+
+    def __init__(self, *mods):
+        super().__init__()
+        self.mods = mods
+        for idx, mod in enumerate(mods):
+            self.add_module(str(idx), mod)
+
+    def layers(self):
+        return sum(mod.layers() for mod in self.mods)
+
+
+class Mixture(NNGPKernel):
+    """kernels.py:203-229 — softmax(logit)-weighted sum of branches."""
+
+    def __init__(self, mods, logit_proportions=None):
+        super().__init__()
+        self.mods = mods
+        for idx, mod in enumerate(mods):
+            self.add_module(str(idx), mod)
+        if logit_proportions is None:
+            logit_proportions = torch.zeros(len(mods))
+        self.logit = nn.Parameter(logit_proportions)
+
+    def proportions(self):
+        """softmax of the logits in their own dtype (kernels.py:221), as floats."""
+        with torch.no_grad():
+            lg = self.logit.detach().cpu()
+            return [float(v) for v in torch.softmax(lg, dim=0)]
+
+    def layers(self):
+        return max(mod.layers() for mod in self.mods)
+
+
+class Sum(NNGPKernel):
+    """kernels.py:246-260 — elementwise sum of the branches' outputs."""
+
+    def __init__(self, mods):
+        super().__init__()
+        self.mods = mods
+        for idx, mod in enumerate(mods):
+            self.add_module(str(idx), mod)
+
+    def layers(self):
+        return max(mod.layers() for mod in self.mods)
+
+
+def resnet_block(stride=1, projection_shortcut=False, multiplier=1):
+    """kernels.py:274-296."""
+    if stride == 1 and not projection_shortcut:
+        return Sum([
+            Sequential(),
+            Sequential(
+                ReLU(),
+                Conv2d(3, stride=stride, in_channel_multiplier=multiplier,
+                       out_channel_multiplier=multiplier),
+                ReLU(),
+                Conv2d(3, in_channel_multiplier=multiplier, out_channel_multiplier=multiplier),
+            )
+        ])
+    return Sequential(
+        ReLU(),
+        Sum([
+            Conv2d(1, stride=stride, in_channel_multiplier=multiplier // stride,
+                   out_channel_multiplier=multiplier),
+            Sequential(
+                Conv2d(3, stride=stride, in_channel_multiplier=multiplier // stride,
+                       out_channel_multiplier=multiplier),
+                ReLU(),
+                Conv2d(3, in_channel_multiplier=multiplier, out_channel_multiplier=multiplier),
+            )
+        ]),
+    )
+

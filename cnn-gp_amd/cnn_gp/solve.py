@@ -1,0 +1,134 @@
+"""GP solve and classification on the device (reference:
+exp_mnist_resnet/classify_gp.py:17-48).
+
+``solve_system`` is ``scipy.linalg.solve(Kxx, Y, assume_a='pos', lower=False)`` done by
+rocSOLVER: Cholesky (dpotrf_64) on the UPPER triangle of the row-major Kxx — the only
+triangle the reference's HDF5 files fill — then dpotrs_64.  All through libcnngp.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+__all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
+           "accuracy", "one_hot_pm1")
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("cnn_gp solve needs a HIP device (there is no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = True):
+    """Kxx⁻¹ Y for symmetric positive-definite Kxx given by its upper triangle.
+
+    Kxx, Y: float64 tensors (classify_gp.py:19-23 asserts the same), on the host or the
+    device.  Kxx is overwritten with its Cholesky factor when it already lives on the
+    device and ``overwrite_a`` (the reference passes overwrite_a=True).  Returns the
+    solution on Y's device.  Raises ``np.linalg.LinAlgError`` if Kxx (+ jitter·I) is not
+    positive definite, like scipy.
+    """
+    assert Kxx.dtype == torch.float64 and Y.dtype == torch.float64, """
+    It is important that `Kxx` and `Y` are `float64`s for the inversion,
+    even if they were `float32` when being calculated."""
+    n = Kxx.shape[0]
+    assert Kxx.dim() == 2 and Kxx.shape[1] == n and Y.shape[0] == n
+    vec = Y.dim() == 1
+    Y2 = Y.reshape(n, -1)
+    dev = Kxx.device if Kxx.device.type == "cuda" else _device()
+    with torch.cuda.device(dev):
+        if Kxx.device == dev and overwrite_a and Kxx.is_contiguous():
+            K = Kxx
+        elif Kxx.device == dev:
+            K = Kxx.clone(memory_format=torch.contiguous_format)
+        else:
+            K = Kxx.to(dev).contiguous()
+        yd = Y2.to(dev).contiguous()
+        nrhs = yd.shape[1]
+        bt = torch.empty((nrhs, n), dtype=torch.float64, device=dev)
+        s = _stream(dev)
+        N.call("cgp_transpose_f64", N.ptr(yd), n, nrhs, N.ptr(bt), s)
+        info = N._i64(0)
+        N.check(N.load().cgp_chol_solve_f64(N.ptr(K), n, n, N.ptr(bt), nrhs, n, float(jitter),
+                                            ctypes.byref(info), s), "cgp_chol_solve_f64")
+        if info.value > 0:
+            raise np.linalg.LinAlgError(
+                f"Kxx is not positive definite (leading minor of order {info.value})")
+        sol = torch.empty((n, nrhs), dtype=torch.float64, device=dev)
+        N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
+    sol = sol.reshape(n) if vec else sol
+    return sol.to(Y.device)
+
+
+def diag_add(K, diag):
+    """K[i, i] += diag in place (classify_gp.py:30-36)."""
+    if isinstance(K, torch.Tensor):
+        K.view(K.numel())[::K.shape[-1] + 1] += diag
+    elif isinstance(K, np.ndarray):
+        K.flat[::K.shape[-1] + 1] += diag
+    else:
+        raise TypeError("What do I do with a `{}`, K={}?".format(type(K), K))
+
+
+def load_kern(dset, i, device=None):
+    """dataset[i] (float32) -> float64 tensor (classify_gp.py:45-48); widened on the
+    device when ``device`` is a cuda device."""
+    A = np.empty(dset.shape[1:], dtype=np.float32)
+    if hasattr(dset, "read_direct"):
+        dset.read_direct(A, source_sel=np.s_[i, :, :])
+    else:
+        A[...] = np.asarray(dset[i])
+    t = torch.from_numpy(A)
+    if device is None or torch.device(device).type != "cuda":
+        return t.to(dtype=torch.float64)
+    dev = torch.device(device)
+    with torch.cuda.device(dev):
+        src = t.to(dev)
+        out = torch.empty(src.shape, dtype=torch.float64, device=dev)
+        N.call("cgp_cast_f32_f64", N.ptr(src), N.ptr(out), src.numel(), _stream(dev))
+    return out
+
+
+def predict(A, Kxz):
+    """argmax over classes of Kxz @ A (classify_gp.py:39-40), on the device."""
+    dev = Kxz.device if Kxz.device.type == "cuda" else _device()
+    with torch.cuda.device(dev):
+        K = Kxz.to(dev, dtype=torch.float64).contiguous()
+        Ad = A.to(dev, dtype=torch.float64).contiguous()
+        m, kdim = K.shape
+        ncls = Ad.shape[1]
+        scores = torch.empty((m, ncls), dtype=torch.float64, device=dev)
+        s = _stream(dev)
+        N.call("cgp_gemm_f64", N.ptr(K), N.ptr(Ad), N.ptr(scores), m, ncls, kdim, s)
+        pred = torch.empty((m,), dtype=torch.int64, device=dev)
+        N.call("cgp_argmax_rows_f64", N.ptr(scores), m, ncls, N.ptr(pred), s)
+    return pred
+
+
+def accuracy(pred, Y) -> float:
+    Yt = torch.as_tensor(Y).reshape(-1).cpu()
+    return float((pred.cpu() == Yt).double().mean())
+
+
+def print_accuracy(A, Kxvx, Y, key):
+    acc = accuracy(predict(A, Kxvx), Y)
+    print(f"{key} accuracy: {acc*100}%")
+    return acc
+
+
+def one_hot_pm1(labels, n_classes=None):
+    """Y_1hot of classify_gp.py:56-59: -1 everywhere, +1 at each label, float64."""
+    labels = torch.as_tensor(labels)
+    n_classes = int(labels.max()) + 1 if n_classes is None else n_classes
+    Y = torch.ones((len(labels), n_classes), dtype=torch.float64).neg_()
+    Y[torch.arange(len(labels)), labels] = 1.
+    return Y

@@ -1,0 +1,187 @@
+/*
+ * cnngp.h — C ABI of the MI355X-native CNN-GP hot path (libcnngp.so).
+ *
+ * The reference (waleedbinkhalid74/cnn-gp) is pure Python over PyTorch; it has no FFI of
+ * its own.  Each entry point below replaces the PyTorch op sequence one reference
+ * function issues, so a ctypes (or any C FFI) binding can drive the whole NNGP Gram
+ * recursion and the GP solve without torch compute.  Citations are
+ * /root/reference/<file>:<line>.
+ *
+ * Conventions
+ *   - Every buffer is DEVICE memory owned by the caller (torch allocates it and passes
+ *     data_ptr()).  The library never frees caller memory.  rocBLAS / rocSOLVER handles
+ *     are owned by the library, cached per device.
+ *   - Every compute entry point is asynchronous on `stream` (a hipStream_t passed as
+ *     void*; NULL = the null stream).  No host synchronisation inside, except the solve,
+ *     which returns potrf's `info` to the host.
+ *   - Return value: 0 on success, otherwise a CGP_E* code; cgp_last_error() returns a
+ *     thread-local message for the last failure.  No C++ exception crosses the ABI.
+ *   - Layouts are row-major and dense.  A "map" is one H×W spatial plane.  The pair
+ *     index of a non-diagonal tile is m = i·N2 + j (i over the N1 rows, j over the N2
+ *     columns); for a diagonal (diag=1) tile m = i = j.
+ *   - _f64 entry points compute in double, _f32 in float (the reference's production
+ *     dtype).  Scalars (weight, bias) are passed as double and rounded to the compute
+ *     type inside the f32 entry points.
+ */
+#ifndef CNNGP_H
+#define CNNGP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGP_ABI_VERSION 1
+
+/* error codes */
+#define CGP_OK 0
+#define CGP_EINVAL 1001   /* argument check failed (shapes, null pointers, ranges) */
+#define CGP_EHIP 1002     /* a HIP runtime call or kernel launch failed */
+#define CGP_EBLAS 1003    /* rocBLAS / rocSOLVER returned an error status */
+
+/* cgp_conv_args.pre / .post */
+#define CGP_PRE_NONE 0
+#define CGP_PRE_RELU 1     /* apply the ReLU covariance map to the input while staging it */
+#define CGP_PRE_MOMENTS 2  /* the input is (x, y) images; stage mean_c x·y instead of a map */
+#define CGP_POST_NONE 0
+#define CGP_POST_RELU 1    /* apply the ReLU covariance map to the conv output */
+
+int cgp_abi_version(void);
+const char* cgp_last_error(void);
+/* sizeof of the argument structs, so an FFI can verify its mirror of the layout */
+size_t cgp_conv_args_size(void);
+size_t cgp_relu_args_size(void);
+/* number of visible HIP devices (0 without a GPU; never fails) */
+int cgp_device_count(void);
+
+/*
+ * Input moments — replaces NNGPKernel.forward's moment step, kernels.py:44-49:
+ *   xy[m] = mean_c x[i,c]·y[j,c]   (diag: xy[i] = mean_c x[i,c]·y[i,c])
+ * x: [n1][c][hw], y: [n2][c][hw]; xy: [n1·n2][hw] (diag: [n1][hw]).
+ */
+int cgp_moments_xy_f64(const double* x, const double* y, int64_t n1, int64_t n2,
+                       int32_t c, int32_t hw, int32_t diag, double* xy, void* stream);
+int cgp_moments_xy_f32(const float* x, const float* y, int64_t n1, int64_t n2,
+                       int32_t c, int32_t hw, int32_t diag, float* xy, void* stream);
+/*
+ * Per-image variances — kernels.py:48-49: xx[i] = mean_c x[i,c]², yy[j] = mean_c y[j,c]².
+ * Writes xx: [n1][hw] and yy: [n2][hw] (they may be one contiguous [n1+n2][hw] block).
+ */
+int cgp_moments_var_f64(const double* x, const double* y, int64_t n1, int64_t n2,
+                        int32_t c, int32_t hw, double* xx, double* yy, void* stream);
+int cgp_moments_var_f32(const float* x, const float* y, int64_t n1, int64_t n2,
+                        int32_t c, int32_t hw, float* xx, float* yy, void* stream);
+
+/*
+ * Conv2d covariance stencil — replaces Conv2d.propagate, kernels.py:92-98
+ * (F.conv2d with the constant kernel of kernels.py:78-88, then + var_bias):
+ *   out[m,oh,ow] = weight · Σ_{a,b<taps} in[m, oh·s+off+a·d, ow·s+off+b·d] + bias
+ * with zero padding outside [0,h)×[0,w).  `offset` is -padding, plus `dilation` when the
+ * reference pads an even kernel to (k+1)² with a zero first row/column (kernels.py:73-84).
+ * Optional fusions (one HBM pass instead of two or three):
+ *   pre  = CGP_PRE_RELU:    the staged input is ReLU.propagate(in) (kernels.py:134-165),
+ *                           using pre_xx/pre_yy = the variances at the ReLU's input;
+ *   pre  = CGP_PRE_MOMENTS: the staged input is mean_c x·y of in (=x) and in_y (=y);
+ *   post = CGP_POST_RELU:   out is ReLU.propagate of the conv output, using
+ *                           post_xx/post_yy = the variances of the conv output;
+ *   addend != NULL:         out += addend after everything else (Sum, kernels.py:252-254,
+ *                           kernel_patch.py:43-63).
+ * Variance maps (pre_xx etc.) are [n1][h·w] / [n2][h·w] at the resolution they apply to.
+ */
+typedef struct cgp_conv_args {
+    const void* in;       /* [nmaps][h][w]; or x [n1][channels][h][w] with CGP_PRE_MOMENTS */
+    const void* in_y;     /* y [n2][channels][h][w] with CGP_PRE_MOMENTS, else NULL */
+    void* out;            /* [nmaps][ho][wo] */
+    const void* addend;   /* [nmaps][ho][wo] or NULL */
+    const void* pre_xx;   /* CGP_PRE_RELU: [n1][h][w] */
+    const void* pre_yy;   /* CGP_PRE_RELU: [n2][h][w] */
+    const void* post_xx;  /* CGP_POST_RELU: [n1][ho][wo] */
+    const void* post_yy;  /* CGP_POST_RELU: [n2][ho][wo] */
+    int64_t nmaps;        /* n1·n2, or n1 when diag */
+    int64_t n1, n2;
+    int32_t h, w, ho, wo;
+    int32_t taps, offset, stride, dilation;
+    int32_t channels;     /* CGP_PRE_MOMENTS only */
+    int32_t pre, post;
+    int32_t same, diag;   /* KernelPatch.same / .diag (kernel_patch.py:4-30) */
+    int32_t maps_per_block; /* 0 = library default */
+    double weight, bias;
+} cgp_conv_args;
+int cgp_conv_f64(const cgp_conv_args* args, void* stream);
+int cgp_conv_f32(const cgp_conv_args* args, void* stream);
+
+/*
+ * ReLU covariance map on the pair maps — ReLU.propagate, kernels.py:134-165:
+ *   t = xx[i]·yy[j] + f32_tiny; cos = clamp(xy·rsqrt(t), -1, 1);
+ *   sin = sqrt(max(t - xy², 0)); out = (sin + (π - acos(cos))·xy) / 2π
+ * same && !diag: out[i,i] = xx[i]/2; same && diag: out = xx/2.  Optional out += addend.
+ * In-place (out == xy) is allowed.
+ */
+typedef struct cgp_relu_args {
+    const void* xy;      /* [nmaps][hw] */
+    void* out;           /* [nmaps][hw] */
+    const void* addend;  /* [nmaps][hw] or NULL */
+    const void* xx;      /* [n1][hw] variances at the ReLU input */
+    const void* yy;      /* [n2][hw] */
+    int64_t nmaps, n1, n2;
+    int32_t hw, same, diag, reserved;
+} cgp_relu_args;
+int cgp_relu_f64(const cgp_relu_args* args, void* stream);
+int cgp_relu_f32(const cgp_relu_args* args, void* stream);
+
+/*
+ * ReLU on the per-image variances — kernels.py:154-164: xx' = xx/2;
+ * yy' = xx' if same else yy/2.  xx: [n1][hw], yy: [n2][hw].
+ */
+int cgp_var_relu_f64(const double* xx, const double* yy, int64_t n1, int64_t n2, int32_t hw,
+                     int32_t same, double* xx_out, double* yy_out, void* stream);
+int cgp_var_relu_f32(const float* xx, const float* yy, int64_t n1, int64_t n2, int32_t hw,
+                     int32_t same, float* xx_out, float* yy_out, void* stream);
+
+/*
+ * out = alpha·a + beta·b (b may be NULL: out = alpha·a), n elements.  The unfused form
+ * of Sum (alpha = beta = 1, kernel_patch.py:43-63) and Mixture (kernels.py:220-225).
+ * Products and the sum are rounded separately (no FMA contraction), like torch.
+ */
+int cgp_axpby_f64(double alpha, const double* a, double beta, const double* b, double* out,
+                  int64_t n, void* stream);
+int cgp_axpby_f32(double alpha, const float* a, double beta, const float* b, float* out,
+                  int64_t n, void* stream);
+
+/* load_kern's float32 → float64 widening, classify_gp.py:45-48 */
+int cgp_cast_f32_f64(const float* in, double* out, int64_t n, void* stream);
+/* dst[c][r] = src[r][c]; src [rows][cols] row-major */
+int cgp_transpose_f64(const double* src, int64_t rows, int64_t cols, double* dst, void* stream);
+
+/*
+ * GP solve — replaces classify_gp.solve_system + diag_add (classify_gp.py:17-36):
+ * scipy.linalg.solve(K, Y, assume_a='pos', lower=False) reads only the UPPER triangle
+ * of the row-major K (its strictly-lower tiles are NaN in the reference's HDF5 files).
+ *   K:  [n][ldk] row-major fp64; overwritten by the Cholesky factor (rocsolver_dpotrf_64
+ *       on the column-major view = lower, i.e. the row-major upper triangle).
+ *   bt: the right-hand sides TRANSPOSED, [nrhs][ldb] row-major (= column-major n×nrhs);
+ *       overwritten by the solution (transposed).
+ *   jitter is added to K's diagonal first (diag_add, classify_gp.py:30-36).
+ *   *info (host): 0 = success; > 0 = the leading minor of that order is not positive
+ *   definite (scipy raises LinAlgError in that case).
+ * Synchronises `stream` before returning.
+ */
+int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
+                       int64_t ldb, double jitter, int64_t* info, void* stream);
+/*
+ * Row-major C[m][n] = A[m][kdim] @ B[kdim][n] (fp64, rocBLAS) — the Kxz @ α product of
+ * print_accuracy, classify_gp.py:39-42.
+ */
+int cgp_gemm_f64(const double* a, const double* b, double* c, int64_t m, int64_t n,
+                 int64_t kdim, void* stream);
+/* out[r] = argmax_c a[r][c] (first maximum, like torch.argmax), a: [rows][cols] */
+int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* out,
+                        void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CNNGP_H */

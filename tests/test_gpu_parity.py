@@ -1,0 +1,330 @@
+"""GPU parity: the HIP path (through libcnngp.so) against the reference's golden vectors
+and the CPU oracle.  Tolerances: float64 1e-10 relative on kernel entries (north star:
+1e-5); float32 2e-5 relative against the reference's own float32 run."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import cnn_gp
+from cnn_gp import _native as N
+from oracle import nngp_oracle as O
+from oracle import specs
+
+from conftest import GOLDEN
+import configs_util
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+RTOL64 = 1e-10
+RTOL32 = 2e-5
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dev(a, dt=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dt)
+
+
+def rel_err(got, ref):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    return float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)))
+
+
+# ------------------------------------------------------------------------------------
+# Conv2d covariance stencil against the reference's Conv2d.propagate
+# ------------------------------------------------------------------------------------
+def conv_direct(maps, spec, pre=0, post=0, addend=None, pre_var=None, post_var=None,
+                n1=None, n2=None, same=0, diag=0, mpb=0, dtype=torch.float64):
+    g = O.conv_geometry(spec)
+    P, H, W = maps.shape
+    Ho, Wo = O.conv_out_size(H, g), O.conv_out_size(W, g)
+    x = dev(maps, dtype)
+    out = torch.empty((P, Ho, Wo), dtype=dtype, device=DEV)
+    a = N.ConvArgs()
+    a.in_, a.out = N.ptr(x), N.ptr(out)
+    a.nmaps, a.n1, a.n2 = P, n1 or P, n2 or 1
+    a.h, a.w, a.ho, a.wo = H, W, Ho, Wo
+    a.taps = g["k"]
+    a.offset = -g["pad"] + (g["d"] if g["zero_row"] else 0)
+    a.stride, a.dilation = g["s"], g["d"]
+    a.weight = float(O.conv_weight(spec, np.float64))
+    a.bias = float(spec.get("var_bias", 0.0))
+    a.pre, a.post, a.same, a.diag, a.maps_per_block = pre, post, same, diag, mpb
+    keep = []
+    if addend is not None:
+        t = dev(addend, dtype)
+        keep.append(t)
+        a.addend = N.ptr(t)
+    if pre_var is not None:
+        vx, vy = dev(pre_var[0], dtype), dev(pre_var[1], dtype)
+        keep += [vx, vy]
+        a.pre_xx, a.pre_yy = N.ptr(vx), N.ptr(vy)
+    if post_var is not None:
+        vx, vy = dev(post_var[0], dtype), dev(post_var[1], dtype)
+        keep += [vx, vy]
+        a.post_xx, a.post_yy = N.ptr(vx), N.ptr(vy)
+    fn = N.load().cgp_conv_f64 if dtype == torch.float64 else N.load().cgp_conv_f32
+    N.check(fn(ctypes.byref(a), stream()), "cgp_conv")
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def par_spec(par):
+    k, s, pad, d, vw, vb = par
+    return dict(kernel_size=int(k), stride=int(s), padding="same" if pad == -1 else int(pad),
+                dilation=int(d), var_weight=float(vw), var_bias=float(vb))
+
+
+def test_conv_golden_cases():
+    z = load("conv_ops.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in z.files})
+    worst = 0.0
+    for k in keys:
+        spec = par_spec(z[k + "_par"])
+        got = conv_direct(z[k + "_in"].astype(np.float64), spec)
+        ref = z[k + "_out"]
+        assert got.shape == ref.shape, k
+        err = rel_err(got, ref)
+        worst = max(worst, err)
+        assert err < 1e-13, (k, spec, err)
+    print("worst conv rel err", worst)
+
+
+@pytest.mark.parametrize("mpb", [1, 3, 7, 0])
+def test_conv_chunking_and_ragged_tail(mpb):
+    rng = np.random.default_rng(mpb)
+    maps = rng.random((37, 14, 14))
+    spec = dict(kernel_size=3, stride=2, padding="same", dilation=1, var_weight=3.0,
+                var_bias=0.25)
+    got = conv_direct(maps, spec, mpb=mpb)
+    np.testing.assert_allclose(got, O.conv_maps(maps, spec), rtol=1e-14, atol=0)
+
+
+def _pair_kp(n1, n2, side, rng, same=False):
+    X = rng.random((n1, 2, side, side))
+    Y = X if same else rng.random((n2, 2, side, side))
+    return O.moments(X, Y, same, False), X, Y
+
+
+@pytest.mark.parametrize("same", [False, True])
+def test_fused_pre_relu_post_relu_add(same):
+    rng = np.random.default_rng(5)
+    n1 = 5
+    n2 = 5 if same else 4
+    kp, X, Y = _pair_kp(n1, n2, 12, rng, same)
+    spec = dict(kernel_size=5, stride=1, padding="same", dilation=1, var_weight=2.0,
+                var_bias=0.5)
+    # oracle: conv(relu(kp)) then relu, + addend
+    r1 = O.relu(kp)
+    c = O._conv_kp(r1, spec, "f32")
+    r2 = O.relu(c)
+    addend = rng.random(r2["xy"].shape)
+    ref = r2["xy"] + addend
+    got = conv_direct(kp["xy"], spec, pre=1, post=1, addend=addend,
+                      pre_var=(kp["xx"], kp["yy"]), post_var=(c["xx"], c["yy"]),
+                      n1=n1, n2=n2, same=int(same))
+    assert rel_err(got, ref) < 1e-12
+
+
+def test_fused_moments():
+    rng = np.random.default_rng(6)
+    X = rng.random((4, 3, 9, 9))
+    Y = rng.random((3, 3, 9, 9))
+    spec = dict(kernel_size=3, stride=1, padding="same", dilation=1, var_weight=1.5,
+                var_bias=0.1)
+    kp = O.moments(X, Y, False, False)
+    ref = O.conv_maps(kp["xy"], spec)
+    g = O.conv_geometry(spec)
+    x, y = dev(X), dev(Y)
+    out = torch.empty((12, 9, 9), dtype=torch.float64, device=DEV)
+    a = N.ConvArgs()
+    a.in_, a.in_y, a.out, a.channels = N.ptr(x), N.ptr(y), N.ptr(out), 3
+    a.nmaps, a.n1, a.n2, a.h, a.w, a.ho, a.wo = 12, 4, 3, 9, 9, 9, 9
+    a.taps, a.offset, a.stride, a.dilation = 3, -1, 1, 1
+    a.weight, a.bias, a.pre = float(O.conv_weight(spec, np.float64)), 0.1, N.CGP_PRE_MOMENTS
+    N.check(N.load().cgp_conv_f64(ctypes.byref(a), stream()), "conv")
+    assert rel_err(out.cpu().numpy(), ref) < 1e-13
+    _ = g
+
+
+# ------------------------------------------------------------------------------------
+# ReLU against the reference's ReLU.propagate
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+@pytest.mark.parametrize("same", [0, 1])
+@pytest.mark.parametrize("diag", [0, 1])
+def test_relu_golden(dt, same, diag):
+    z = load("relu_ops.npz")
+    key = f"{dt}_s{same}_d{diag}"
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    xy, xx, yy = z[key + "_xy"], z[key + "_xx"], z[key + "_yy"]
+    n1, hw = xx.shape
+    n2 = yy.shape[0]
+    xyd, xxd, yyd = dev(xy, tdt), dev(xx, tdt), dev(yy, tdt)
+    out = torch.empty_like(xyd)
+    r = N.ReluArgs()
+    r.xy, r.out, r.xx, r.yy = N.ptr(xyd), N.ptr(out), N.ptr(xxd), N.ptr(yyd)
+    r.nmaps, r.n1, r.n2, r.hw, r.same, r.diag = xy.shape[0], n1, n2, hw, same, diag
+    fn = N.load().cgp_relu_f64 if dt == "f64" else N.load().cgp_relu_f32
+    N.check(fn(ctypes.byref(r), stream()), "relu")
+    tol = 1e-12 if dt == "f64" else 2e-6
+    np.testing.assert_allclose(out.cpu().numpy(), z[key + "_oxy"], rtol=tol, atol=tol)
+    xo, yo = torch.empty_like(xxd), torch.empty_like(yyd)
+    sfx = "f64" if dt == "f64" else "f32"
+    N.call(f"cgp_var_relu_{sfx}", N.ptr(xxd), N.ptr(yyd), n1, n2, hw, same, N.ptr(xo),
+           N.ptr(yo), stream())
+    np.testing.assert_array_equal(xo.cpu().numpy(), z[key + "_oxx"])
+    np.testing.assert_array_equal(yo.cpu().numpy(), z[key + "_oyy"])
+
+
+def test_relu_known_answers():
+    z = load("relu_ops.npz")
+    c, v1, v2 = dev(z["known_c"]), dev(z["known_v1"]), dev(z["known_v2"])
+    out = torch.empty_like(c)
+    r = N.ReluArgs()
+    r.xy, r.out, r.xx, r.yy = N.ptr(c), N.ptr(out), N.ptr(v1), N.ptr(v2)
+    r.nmaps, r.n1, r.n2, r.hw, r.same, r.diag = 4, 4, 4, 1, 0, 1
+    N.check(N.load().cgp_relu_f64(ctypes.byref(r), stream()), "relu")
+    o = out.cpu().numpy()
+    np.testing.assert_allclose(o, z["known_out"], rtol=1e-12, atol=0)
+    assert abs(o[3] - 1.7255613506e-20) / 1.7255613506e-20 < 1e-9   # sqrt(f32 tiny)/2π
+
+
+# ------------------------------------------------------------------------------------
+# end to end against the reference's own outputs
+# ------------------------------------------------------------------------------------
+CFGS = ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp", "mnist_as_tf", "cifar10"]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("dtn", ["f64", "f32"])
+def test_e2e_matches_reference_golden(cfg, dtn):
+    z = load(f"e2e_{cfg}.npz")
+    tdt = torch.float64 if dtn == "f64" else torch.float32
+    model = configs_util.model(cfg).to(DEV, tdt)
+    tol = RTOL64 if dtn == "f64" else RTOL32
+    prefixes = sorted({k.rsplit("_", 1)[0] for k in z.files if k.endswith("_X")})
+    for pre in prefixes:
+        X, Z = dev(z[pre + "_X"], tdt), dev(z[pre + "_Z"], tdt)
+        with torch.no_grad():
+            got = {
+                "Kxx": model(X),
+                "Kxz": model(X, Z, False, False),
+                "Kxdiag": model(X, X, True, True),
+                "Kxzdiag": model(X[:6], Z, False, True),
+            }
+        for name, t in got.items():
+            assert t.dtype == tdt and t.device.type == "cuda"
+            err = rel_err(t.cpu().numpy(), z[f"{pre}_{dtn}_{name}"])
+            assert err < tol, (cfg, pre, dtn, name, err)
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+def test_fusion_is_exact(cfg):
+    """the fused program and the op-by-op program give identical results"""
+    rng = np.random.default_rng(3)
+    C, side = specs.GEOMETRY[cfg]
+    X = dev(rng.random((5, C, side, side)))
+    Z = dev(rng.random((3, C, side, side)))
+    m = configs_util.model(cfg).to(DEV, torch.float64)
+    with torch.no_grad():
+        a = m(X, Z, False, False).cpu().numpy()
+        b = m.set_fusion(False)(X, Z, False, False).cpu().numpy()
+    assert rel_err(a, b) < 1e-13
+
+
+def test_cpu_inputs_round_trip_to_host():
+    z = load("e2e_mnist_paper_convnet_gp.npz")
+    m = configs_util.model("mnist_paper_convnet_gp").double().to(DEV)
+    X = torch.from_numpy(z["s0_mnist_X"]).double()
+    K = m(X)
+    assert K.device.type == "cpu"
+    assert rel_err(K.numpy(), z["s0_mnist_f64_Kxx"]) < RTOL64
+
+
+def test_mixture_against_oracle():
+    spec_m = cnn_gp.Sequential(
+        cnn_gp.Conv2d(3, var_bias=0.3),
+        cnn_gp.Mixture([cnn_gp.Sequential(),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3, var_weight=2.0)),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(5))],
+                       torch.tensor([0.3, -0.2, 0.1])),
+        cnn_gp.ReLU(), cnn_gp.Conv2d(10, padding=0))
+    rng = np.random.default_rng(8)
+    X = rng.random((4, 1, 10, 10))
+    Z = rng.random((3, 1, 10, 10))
+    ref = O.kernel(configs_util.spec_of(spec_m), X, Z, False, False)
+    got = spec_m.double().to(DEV)(dev(X), dev(Z), False, False).cpu().numpy()
+    assert rel_err(got, ref) < 1e-6     # softmax: torch (product) vs numpy (oracle)
+
+
+# ------------------------------------------------------------------------------------
+# edge cases and size-independent properties
+# ------------------------------------------------------------------------------------
+def test_edge_shapes_and_zero_images():
+    m = configs_util.model("mnist_as_tf").double().to(DEV)
+    spec = specs.mnist_as_tf()
+    rng = np.random.default_rng(2)
+    X = rng.random((3, 1, 28, 28))
+    X[1] = 0.0                                  # an all-zero image: f32_tiny path
+    for n1, n2 in [(1, 1), (1, 3), (3, 1)]:
+        a, b = X[:n1], X[-n2:]
+        ref = O.kernel(spec, a, b, False, False)
+        got = m(dev(a), dev(b), False, False).cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-300)
+    ref = O.kernel(spec, X)
+    got = m(dev(X)).cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-300)
+    # same-tile diagonal override: K[1,1] = xx/2 chain of a zero image is exactly 0;
+    # off the diagonal the f32_tiny term keeps zero-variance pairs strictly positive
+    assert got[1, 1] == ref[1, 1] == 0.0
+    assert np.isfinite(got).all() and (got[1, [0, 2]] > 0).all()
+
+
+def test_tiles_assemble_to_full_matrix_and_symmetry():
+    """tile vs full: same=False tiles of Kxx equal the full same=True evaluation except
+    on the diagonal (override), and Kxx is symmetric + positive definite"""
+    m = configs_util.model("mnist_paper_convnet_gp").double().to(DEV)
+    rng = np.random.default_rng(4)
+    X = dev(rng.random((24, 1, 28, 28)))
+    full = m(X).cpu().numpy()
+    assert np.array_equal(full, full.T) or rel_err(full, full.T) < 1e-15
+    top = m(X[:12], X[12:], False, False).cpu().numpy()
+    np.testing.assert_allclose(top, full[:12, 12:], rtol=1e-15)
+    np.linalg.cholesky(full)
+
+
+def test_solve_golden_nan_lower():
+    z = load("solve.npz")
+    K = torch.from_numpy(z["K"].copy())
+    K[tuple(np.tril_indices(len(K), -1))] = float("nan")
+    Y = torch.from_numpy(z["Y"])
+    sol = cnn_gp.solve_system(K.to(DEV), Y.to(DEV), jitter=float(z["jitter"]))
+    np.testing.assert_allclose(sol.cpu().numpy(), z["sol"], rtol=1e-9, atol=1e-9)
+
+
+def test_solve_not_pd_raises():
+    K = torch.tensor([[1.0, 2.0], [2.0, 1.0]], dtype=torch.float64, device=DEV)
+    with pytest.raises(np.linalg.LinAlgError):
+        cnn_gp.solve_system(K, torch.ones(2, 1, dtype=torch.float64, device=DEV))
+
+
+def test_predict_and_cast():
+    rng = np.random.default_rng(9)
+    Kxz = rng.random((50, 40))
+    A = rng.standard_normal((40, 10))
+    pred = cnn_gp.predict(dev(A), dev(Kxz)).cpu().numpy()
+    np.testing.assert_array_equal(pred, np.argmax(Kxz @ A, axis=1))
+    f32 = rng.random((3, 7, 5)).astype(np.float32)
+    out = cnn_gp.load_kern(f32, 1, device=DEV)
+    np.testing.assert_array_equal(out.cpu().numpy(), f32[1].astype(np.float64))

@@ -1,0 +1,243 @@
+"""CPU-only tests: the C ABI library loads and exports what include/cnngp.h declares,
+the program compiler/fuser, the tile schedule and HDF5 layout, and the host plumbing."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import cnn_gp
+from cnn_gp import _native as N
+from cnn_gp.program import Plan
+from cnn_gp.data import tile_schedule, worker_slice, read_idx, ProductIterator
+from cnn_gp.kernel_save_tools import save_K, merge_nan_fill
+from oracle import nngp_oracle as O
+from oracle import specs
+
+from conftest import ROOT, GOLDEN
+import configs_util
+
+
+HEADER = os.path.join(ROOT, "include", "cnngp.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(cgp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = N.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(N.SIGNATURES), set(syms) ^ set(N.SIGNATURES)
+
+
+def test_struct_layouts_match():
+    lib = N.load()
+    assert lib.cgp_conv_args_size() == ctypes.sizeof(N.ConvArgs)
+    assert lib.cgp_relu_args_size() == ctypes.sizeof(N.ReluArgs)
+    assert lib.cgp_abi_version() == N.CGP_ABI_VERSION
+
+
+def test_device_count_without_gpu_is_safe():
+    assert N.load().cgp_device_count() >= 0
+
+
+def test_invalid_arguments_rejected_on_host():
+    """argument checks run before any launch (no GPU needed to exercise them)"""
+    lib = N.load()
+    a = N.ConvArgs()
+    assert lib.cgp_conv_f64(ctypes.byref(a), None) == 1001
+    assert b"NULL" in lib.cgp_last_error()
+    a.in_, a.out = 16, 32
+    a.nmaps, a.h, a.w, a.ho, a.wo = 4, 28, 28, 30, 28
+    a.taps, a.offset, a.stride, a.dilation = 3, -1, 1, 1
+    assert lib.cgp_conv_f64(ctypes.byref(a), None) == 1001
+    assert b"inconsistent" in lib.cgp_last_error()
+    r = N.ReluArgs()
+    assert lib.cgp_relu_f64(ctypes.byref(r), None) == 1001
+    assert lib.cgp_axpby_f64(1.0, None, 1.0, None, None, 10, None) == 1001
+
+
+def test_forward_without_gpu_fails_loudly():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    m = cnn_gp.Sequential(cnn_gp.Conv2d(3), cnn_gp.ReLU(), cnn_gp.Conv2d(4, padding=0))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.rand(2, 1, 4, 4, dtype=torch.float64))
+
+
+# ------------------------------------------------------------------------------------
+# program compiler
+# ------------------------------------------------------------------------------------
+def _kinds(plan):
+    return [(o.kind, o.pre, o.post, o.addend is not None) for o in plan.pair_ops]
+
+
+def test_convnet_fuses_to_eight_kernels():
+    m = configs_util.model("mnist_paper_convnet_gp")
+    p = Plan(m, 28, 28)
+    k = _kinds(p)
+    assert len(k) == 8
+    assert k[0] == ("conv", N.CGP_PRE_MOMENTS, N.CGP_POST_RELU, False)
+    assert all(x == ("conv", 0, 1, False) for x in k[1:7])
+    assert k[7] == ("conv", 0, 0, False)
+    assert p.final_hw == (1, 1) and p.moments_fused
+
+
+def test_resnet_fusion_counts():
+    m = configs_util.model("mnist_as_tf")
+    p = Plan(m, 28, 28)
+    unfused = Plan(m, 28, 28, enable_fusion=False)
+    assert len(unfused.pair_ops) == 36 + 31 + 15
+    # identity block -> 2 kernels; projection block -> relu + conv1 + conv3(post) +
+    # conv3(add), except the first, whose relu folds into the stem conv's epilogue
+    assert len(p.pair_ops) == 1 + 3 * (4 + 4 * 2) - 1 + 2
+    assert sum(o.kind == "relu" for o in p.pair_ops) == 2
+    assert not any(o.kind == "add" for o in p.pair_ops)
+
+
+def test_residual_cnn_gp_fusion():
+    m = configs_util.model("mnist_paper_residual_cnn_gp")
+    p = Plan(m, 28, 28)
+    k = _kinds(p)
+    # 8 x [conv4 + relu + add(identity)] -> 1 kernel each, then conv4+relu, final conv
+    assert len(k) == 8 + 1 + 1
+    assert not p.moments_fused   # v0 feeds both the first conv and the first shortcut
+    assert sum(1 for x in k if x == ("conv", 0, 1, True)) == 8
+
+
+def test_mixture_lowering_keeps_add():
+    m = cnn_gp.Sequential(cnn_gp.Conv2d(3), cnn_gp.Mixture(
+        [cnn_gp.Sequential(), cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3))],
+        torch.tensor([0.3, -0.2])), cnn_gp.Conv2d(6, padding=0))
+    p = Plan(m, 6, 6)
+    adds = [o for o in p.pair_ops if o.kind == "add"]
+    assert len(adds) == 1 and all(c is not None for c, _ in adds[0].terms)
+
+
+def test_configs_match_oracle_specs():
+    for name in ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp", "mnist_as_tf",
+                 "cifar10"]:
+        assert configs_util.spec_of(configs_util.model(name)) == specs.CONFIGS[name](), name
+
+
+def test_nonsquare_output_error_mentions_size():
+    m = cnn_gp.Sequential(cnn_gp.Conv2d(3))
+    p = Plan(m, 5, 5)
+    assert p.final_hw == (5, 5)
+
+
+# ------------------------------------------------------------------------------------
+# tiles / persistence
+# ------------------------------------------------------------------------------------
+def test_worker_slice_matches_reference_formula():
+    for nb in range(0, 40):
+        for nw in range(1, 9):
+            tot = 0
+            for r in range(nw):
+                s, c = worker_slice(nb, r, nw)
+                assert s == tot
+                tot += c
+            assert tot == nb
+            assert [O.worker_slice(nb, r, nw) for r in range(nw)] == \
+                [worker_slice(nb, r, nw) for r in range(nw)]
+
+
+def test_tile_schedule_matches_oracle():
+    for n, n2, b, nw in [(40, None, 16, 3), (40, 23, 16, 2), (7, None, 3, 4), (100, 64, 32, 5)]:
+        for r in range(nw):
+            ref = O.tile_schedule(n, n2, b, r, nw)
+            got = [(s, i * b, j * b) for s, i, j in tile_schedule(n, n2, b, r, nw)]
+            assert got == ref
+
+
+class FakeDS:
+    def __init__(self, shape, dtype, fillvalue, chunks, maxshape):
+        self.a = np.full(shape, fillvalue, dtype=dtype)
+        self.chunks, self.maxshape, self.shape = chunks, maxshape, shape
+
+    def __setitem__(self, k, v):
+        self.a[k] = v
+
+    def __getitem__(self, k):
+        return self.a[k]
+
+    def __len__(self):
+        return len(self.a)
+
+
+class FakeFile:
+    def __init__(self):
+        self.d = {}
+
+    def keys(self):
+        return self.d.keys()
+
+    def create_dataset(self, name, shape, dtype, fillvalue, chunks, maxshape):
+        self.d[name] = FakeDS(shape, dtype, fillvalue, chunks, maxshape)
+        return self.d[name]
+
+
+def test_save_K_layout_matches_reference_files():
+    """save_K with the oracle as `kern` reproduces the reference's tile files
+    (NaN pattern, chunking, worker split) bit for bit in the NaN mask."""
+    z = np.load(os.path.join(GOLDEN, "tiles.npz"))
+    X, Z = z["X"].astype(np.float64), z["Z"].astype(np.float64)
+    spec = specs.mnist_paper_convnet_gp()
+    dsx = torch.utils.data.TensorDataset(torch.from_numpy(X), torch.zeros(len(X)))
+    dsz = torch.utils.data.TensorDataset(torch.from_numpy(Z), torch.zeros(len(Z)))
+
+    def kern(x, x2, same, diag):
+        return O.kernel(spec, x.numpy(), x2.numpy(), same, diag)
+
+    files = []
+    for r in range(3):
+        f = FakeFile()
+        save_K(f, kern, "Kxx", dsx, None, False, 16, worker_rank=r, n_workers=3,
+               print_interval=1e9)
+        save_K(f, kern, "Kxz", dsx, dsz, False, 16, worker_rank=r, n_workers=3,
+               print_interval=1e9)
+        for name in ("Kxx", "Kxz"):
+            ref = z[f"{name}_nw3_r{r}"]
+            got = f.d[name].a
+            np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+            m = ~np.isnan(ref)
+            np.testing.assert_allclose(got[m], ref[m], rtol=1e-6)
+        assert f.d["Kxx"].chunks == tuple(z["Kxx_chunks_nw3"])
+        files.append(f)
+    merged = merge_nan_fill(files[0].d["Kxx"].a.copy(), [f.d["Kxx"].a for f in files[1:]])
+    ref1 = z["Kxx_nw1_r0"]
+    np.testing.assert_array_equal(np.isnan(merged), np.isnan(ref1))
+    f = FakeFile()
+    save_K(f, kern, "Kx_diag", dsx, None, True, 16, print_interval=1e9)
+    np.testing.assert_allclose(f.d["Kx_diag"].a, z["Kx_diag"], rtol=1e-6)
+    assert f.d["Kx_diag"].chunks == tuple(z["Kx_diag_chunks"])
+    # existing datasets are skipped, like the reference
+    save_K(f, kern, "Kx_diag", dsx, None, True, 16, print_interval=1e9)
+
+
+def test_product_iterator_batches():
+    ds = torch.utils.data.TensorDataset(torch.arange(10.).reshape(10, 1), torch.arange(10))
+    it = ProductIterator(4, ds, None, 0, 1)
+    seen = [(s, i, j, len(a[0]), len(b[0])) for s, (i, a), (j, b) in it]
+    assert seen == [(True, 0, 0, 4, 4), (False, 0, 4, 4, 4), (False, 0, 8, 4, 2),
+                    (True, 4, 4, 4, 4), (False, 4, 8, 4, 2), (True, 8, 8, 2, 2)]
+
+
+def test_idx_reader(tmp_path):
+    imgs = (np.arange(2 * 3 * 4) % 256).astype(np.uint8).reshape(2, 3, 4)
+    raw = bytes([0, 0, 0x08, 3]) + b"".join(int(d).to_bytes(4, "big") for d in imgs.shape)
+    (tmp_path / "t.idx").write_bytes(raw + imgs.tobytes())
+    np.testing.assert_array_equal(read_idx(str(tmp_path / "t.idx")), imgs)
+
+
+def test_print_timings_passthrough(capsys):
+    from cnn_gp.data import print_timings
+    assert list(print_timings([1, 2, 3], print_interval=0.0)) == [1, 2, 3]
+    assert "3/3 it" in capsys.readouterr().out
