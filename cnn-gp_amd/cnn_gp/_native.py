@@ -14,7 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 1
+CGP_ABI_VERSION = 2
+CGP_FLAG_EXACT_RELU = 1
+CGP_FLAG_GENERIC_CONV = 2
 CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
 
@@ -33,7 +35,7 @@ class ConvArgs(ctypes.Structure):
         ("h", _i32), ("w", _i32), ("ho", _i32), ("wo", _i32),
         ("taps", _i32), ("offset", _i32), ("stride", _i32), ("dilation", _i32),
         ("channels", _i32), ("pre", _i32), ("post", _i32), ("same", _i32), ("diag", _i32),
-        ("maps_per_block", _i32),
+        ("maps_per_block", _i32), ("flags", _i32), ("reserved", _i32),
         ("weight", _f64), ("bias", _f64),
     ]
 
@@ -43,7 +45,7 @@ class ReluArgs(ctypes.Structure):
     _fields_ = [
         ("xy", _vp), ("out", _vp), ("addend", _vp), ("xx", _vp), ("yy", _vp),
         ("nmaps", _i64), ("n1", _i64), ("n2", _i64),
-        ("hw", _i32), ("same", _i32), ("diag", _i32), ("reserved", _i32),
+        ("hw", _i32), ("same", _i32), ("diag", _i32), ("flags", _i32),
     ]
 
 
@@ -54,6 +56,7 @@ SIGNATURES = {
     "cgp_conv_args_size": (ctypes.c_size_t, []),
     "cgp_relu_args_size": (ctypes.c_size_t, []),
     "cgp_device_count": (_i32, []),
+    "cgp_selftest": (_i32, []),
     "cgp_moments_xy_f64": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cgp_moments_xy_f32": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cgp_moments_var_f64": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),

@@ -33,10 +33,11 @@ class NNGPKernel(nn.Module):
     def _plan(self, h: int, w: int) -> Plan:
         cache = self.__dict__.setdefault("_cgp_plans", {})
         fusion = getattr(self, "_cgp_fusion", True)
-        key = (h, w, fusion, self._structure_key())
+        exact = getattr(self, "_cgp_exact_relu", False)
+        key = (h, w, fusion, exact, self._structure_key())
         plan = cache.get(key)
         if plan is None:
-            plan = Plan(self, h, w, enable_fusion=fusion)
+            plan = Plan(self, h, w, enable_fusion=fusion, exact_relu=exact)
             cache[key] = plan
         return plan
 
@@ -58,6 +59,14 @@ class NNGPKernel(nn.Module):
         """Enable/disable op fusion in the pair pipeline (for A/B tests; default on)."""
         for m in self.modules():
             m.__dict__["_cgp_fusion"] = bool(enabled)
+        return self
+
+    def set_exact_relu(self, enabled: bool):
+        """Evaluate the ReLU map op by op exactly like the reference (correctly rounded
+        1/sqrt, sqrt, acos, division) instead of the closed form (default; within 1e-14 of
+        the exact map, see csrc/relu_poly.h).  For parity studies; ~2x slower."""
+        for m in self.modules():
+            m.__dict__["_cgp_exact_relu"] = bool(enabled)
         return self
 
     def forward(self, x, y=None, same=None, diag=False):

@@ -263,7 +263,9 @@ class Plan:
     """A compiled model at one input geometry: the variance program and the fused pair
     program.  Cached per (H, W, fuse) on the model."""
 
-    def __init__(self, model, h: int, w: int, enable_fusion: bool = True):
+    def __init__(self, model, h: int, w: int, enable_fusion: bool = True,
+                 exact_relu: bool = False):
+        self.flags = N.CGP_FLAG_EXACT_RELU if exact_relu else 0
         self.prog, self.v0, self.vf = compile_program(model, h, w)
         self.pair_ops = fuse(self.prog, self.v0, self.vf, enable_fusion)
         self.need_var = needed_variances(self.pair_ops)
@@ -395,6 +397,7 @@ class Plan:
                 a.taps, a.offset, a.stride, a.dilation = g.taps, g.offset, g.stride, g.dilation
                 a.same, a.diag = int(same), int(diag)
                 a.weight, a.bias = g.weight, g.bias
+                a.flags = self.flags
                 fn = getattr(lib, f"cgp_conv_{sfx}")
                 launch = (lambda fn=fn, a=a: N.check(fn(a, stream), "cgp_conv"))
             elif op.kind == "relu":
@@ -406,6 +409,7 @@ class Plan:
                 r.xx, r.yy = N.ptr(vx), N.ptr(vy)
                 r.nmaps, r.n1, r.n2 = nmaps, n1, n2
                 r.hw, r.same, r.diag = ho * wo, int(same), int(diag)
+                r.flags = self.flags
                 fn = getattr(lib, f"cgp_relu_{sfx}")
                 launch = (lambda fn=fn, r=r: N.check(fn(r, stream), "cgp_relu"))
             elif op.kind == "add":

@@ -14,12 +14,14 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
 
 #include "cnngp.h"
+#include "relu_poly.h"
 
 namespace {
 
@@ -53,25 +55,64 @@ int check_launch(const char* what) {
     } while (0)
 
 constexpr int kBlock = 256;          // 4 waves of 64
-constexpr int kChunkElems = 2048;    // target map elements per workgroup chunk
+constexpr int kChunkElems = 2048;    // map elements one workgroup stages per chunk
+constexpr int kEMax = kChunkElems / kBlock;   // prefetch registers per thread (8)
 constexpr int kMaxLds = 64 * 1024;   // bytes of LDS one conv workgroup may take
 
 // ----------------------------------------------------------------------------------
-// the ReLU covariance map (kernels.py:133-152), mirrored op by op: separate roundings
-// (this file is compiled with -ffp-contract=off), torch's clamp NaN propagation,
-// rsqrt as 1/sqrt (ATen's CPU rsqrt), and float constants rounded to T like torch's
-// wrapped Python scalars.
+// n / d for 0 <= n < 2^31 by multiply-high ("division by invariant integers"):
+// q = (umulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1.
+// ----------------------------------------------------------------------------------
+struct FastDiv {
+    unsigned m, s, d;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+    FastDiv f;
+    f.d = d;
+    f.s = 0;
+    while ((1ull << f.s) < d) ++f.s;
+    f.m = (unsigned)(((1ull << 32) * ((1ull << f.s) - d)) / d + 1);
+    return f;
+}
+__host__ __device__ __forceinline__ unsigned umulhi32(unsigned a, unsigned b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umulhi(a, b);
+#else
+    return (unsigned)(((unsigned long long)a * b) >> 32);
+#endif
+}
+__host__ __device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+    return (umulhi32(n, f.m) + n) >> f.s;
+}
+
+// ----------------------------------------------------------------------------------
+// The ReLU covariance map (kernels.py:133-152).
+//
+// relu_exact mirrors the reference op by op: separate roundings (this file is compiled
+// with -ffp-contract=off), torch's clamp NaN propagation, rsqrt as 1/sqrt (ATen's CPU
+// rsqrt), acos, and float constants rounded to T like torch's wrapped Python scalars.
+//
+// relu_fast is the same map in closed form.  With a = |rho| = |c|/sqrt(t) (clamped) and
+// x = (1 - a)/2, acos a = 2 asin sqrt(x) turns (sqrt(t - c²) + (π - acos rho)·c)/2π into
+//     max(c, 0)/2 + sqrt(t) · x · sqrt(x) · P(4x - 1)
+// with P analytic on [0, 1/2] (tools/fit_relu_poly.py; relu_poly.h: degree 15, 3e-15).
+// One branch-free polynomial, two hardware rsq's refined by Newton steps, no division:
+// ~35 double ops instead of ~190 slots for correctly rounded div/sqrt/acos.  Near
+// |rho| = 1 the reference's own acos(rho) is ill-conditioned (~1e-8 relative noise from
+// the last bit of rho); relu_fast evaluates the smooth map there.
 // ----------------------------------------------------------------------------------
 template <typename T> struct K;
 template <> struct K<double> {
     static constexpr double pi = 3.141592653589793;
     static constexpr double two_pi = 6.283185307179586;
     static constexpr double tiny = 1.1754943508222875e-38;   // np.finfo(np.float32).tiny
+    static constexpr double xfloor = 1e-300;
 };
 template <> struct K<float> {
     static constexpr float pi = 3.14159265358979f;
     static constexpr float two_pi = 6.28318530717959f;
     static constexpr float tiny = 1.17549435e-38f;
+    static constexpr float xfloor = 1e-30f;
 };
 
 __device__ __forceinline__ double sqrt_t(double x) { return __builtin_sqrt(x); }
@@ -80,7 +121,7 @@ __device__ __forceinline__ double acos_t(double x) { return acos(x); }
 __device__ __forceinline__ float acos_t(float x) { return acosf(x); }
 
 template <typename T>
-__device__ __forceinline__ T relu_cov(T c, T v1, T v2) {
+__device__ __noinline__ T relu_exact(T c, T v1, T v2) {
     const T t = v1 * v2 + K<T>::tiny;                       // :146
     T cs = c * (T(1) / sqrt_t(t));                          // :149
     cs = cs < T(-1) ? T(-1) : (cs > T(1) ? T(1) : cs);      // clamp(-1, 1), NaN kept
@@ -91,26 +132,76 @@ __device__ __forceinline__ T relu_cov(T c, T v1, T v2) {
     return (s + (K<T>::pi - th) * c) / K<T>::two_pi;        // :152
 }
 
+// rsqrt(t) to full precision: hardware estimate + Newton steps y += y(1 - t y²)/2
+__device__ __forceinline__ double rsqrt_full(double t) {
+    double y = __builtin_amdgcn_rsq(t);
+    double e = __builtin_fma(-t * y, y, 1.0);
+    y = __builtin_fma(0.5 * y, e, y);
+    e = __builtin_fma(-t * y, y, 1.0);
+    return __builtin_fma(0.5 * y, e, y);
+}
+__device__ __forceinline__ float rsqrt_full(float t) {
+    float y = __builtin_amdgcn_rsqf(t);
+    const float e = __builtin_fmaf(-t * y, y, 1.0f);
+    return __builtin_fmaf(0.5f * y, e, y);
+}
+__device__ __forceinline__ double relu_poly(double u) {
+    double r = kReluPolyD[kReluPolyDegD];
+#pragma unroll
+    for (int k = kReluPolyDegD - 1; k >= 0; --k) r = __builtin_fma(r, u, kReluPolyD[k]);
+    return r;
+}
+__device__ __forceinline__ float relu_poly(float u) {
+    float r = kReluPolyF[kReluPolyDegF];
+#pragma unroll
+    for (int k = kReluPolyDegF - 1; k >= 0; --k) r = __builtin_fmaf(r, u, kReluPolyF[k]);
+    return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T relu_fast(T c, T v1, T v2) {
+    const T t = v1 * v2 + K<T>::tiny;
+    const T y = rsqrt_full(t);
+    const T st = t * y;                                     // sqrt(t)
+    T a = c * y;
+    a = a < T(0) ? -a : a;
+    a = a > T(1) ? T(1) : a;                                // |rho| clamped, NaN kept
+    const T x = T(0.5) - T(0.5) * a;                        // (1 - a)/2
+    const T xs = x > K<T>::xfloor ? x : K<T>::xfloor;
+    const T sx = xs * rsqrt_full(xs);                       // sqrt(x)
+    const T p = relu_poly(T(4) * x - T(1));
+    const T pos = c > T(0) ? c : T(0);
+    return (st * x) * sx * p + T(0.5) * pos;
+}
+
 // ReLU of pair map m at pixel px with the same/diag overrides of kernels.py:155-162.
 template <typename T>
 __device__ __forceinline__ T relu_pair(T c, const T* __restrict__ xx, const T* __restrict__ yy,
                                        unsigned i, unsigned j, int hw, int px, int same,
-                                       int diag) {
+                                       int diag, int exact) {
     const T v1 = xx[(size_t)i * hw + px];
     if (same && (diag || i == j)) return v1 / T(2);          // xy' = xx' = xx/2
     const T v2 = yy[(size_t)j * hw + px];
-    return relu_cov(c, v1, v2);
+    return exact ? relu_exact(c, v1, v2) : relu_fast(c, v1, v2);
 }
 
 // pair index -> (i, j)
-__device__ __forceinline__ void pair_of(unsigned m, unsigned n2, int diag, unsigned& i,
+__device__ __forceinline__ void pair_of(unsigned m, const FastDiv& n2, int diag, unsigned& i,
                                         unsigned& j) {
     if (diag) {
         i = j = m;
     } else {
-        i = m / n2;
-        j = m - i * n2;
+        i = fdiv(m, n2);
+        j = m - i * n2.d;
     }
+}
+
+// LDS-only barrier: waits for this wave's LDS traffic, not for its global loads, so the
+// next chunk's prefetch stays in flight across it (cdna_hip_programming.md §5).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
 
 // ----------------------------------------------------------------------------------
@@ -127,128 +218,458 @@ struct ConvP {
     const T* post_xx;
     const T* post_yy;
     long long nmaps;
-    unsigned n2;
+    long long nchunks;
+    FastDiv n2;       // pair index -> (i, j)
+    FastDiv dw;       // in-map element -> row
+    FastDiv dhw;      // chunk element -> map
+    FastDiv dwo;      // output row
+    FastDiv dhowo;    // output map
     int h, w, ho, wo;
-    int taps, off, stride, dil;
+    int hp, wp;       // padded LDS plane (zero halo)
+    int plo_r, plo_c; // halo before row/col 0
+    int c0, r0;       // first tap column / row in the padded plane for output 0
+    int taps, stride, dil;
     int channels;
-    int same, diag;
-    int mpb;        // maps per block
-    int hs_offset;  // element offset of the row-sum plane in LDS
+    int pre, post, add, same, diag, exact;
+    int mpb;          // maps per chunk
+    int hs_offset;    // element offset of the row-sum plane in LDS
     T weight, bias;
 };
 
 // ----------------------------------------------------------------------------------
 // Conv2d covariance stencil, fused (kernels.py:92-98 [+ :134-165 before/after] [+ Sum]).
-// One workgroup = one chunk of `mpb` whole maps:
-//   stage 1  HBM -> LDS   (x the optional PRE op: ReLU or input moments)
-//   stage 2  LDS -> LDS   row sums over the taps        hs[m][r][ow]
-//   stage 3  LDS -> HBM   column sums, ·w + b, optional POST ReLU, optional + addend
+//
+// Persistent workgroups walk chunks of `mpb` whole maps.  Per chunk:
+//   load     HBM -> registers (issued one chunk ahead, in flight during the compute)
+//   stage 1  registers -> LDS, into zero-haloed padded planes (x the PRE op)
+//   stage 2  LDS -> LDS   row sums over the taps, no bounds checks   hs[m][r][ow]
+//   stage 3  LDS -> HBM   column sums, ·w + b, POST ReLU, + addend
 // The constant conv weight makes the k×k stencil separable (2k LDS reads per output
-// instead of k²), and the chunk's input/output are contiguous HBM ranges read and
-// written exactly once.
+// instead of k²); TAPS > 0 unrolls the tap loops.  Every HBM byte is read or written
+// once, with whole-chunk contiguous (coalesced) ranges.
 // ----------------------------------------------------------------------------------
-template <typename T, int PRE, int POST, bool ADD>
-__global__ __launch_bounds__(kBlock) void conv_cov_kernel(const ConvP<T> p) {
+template <typename T, int TAPS>
+__global__ __launch_bounds__(kBlock, 4) void conv_cov_kernel(const ConvP<T> p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* tin = reinterpret_cast<T*>(smem);
     T* ths = tin + p.hs_offset;
-
+    const int tid = threadIdx.x;
     const int hw = p.h * p.w;
     const int howo = p.ho * p.wo;
-    const long long m0 = (long long)blockIdx.x * p.mpb;
-    long long rem = p.nmaps - m0;
-    const int mb = rem < p.mpb ? (int)rem : p.mpb;
-    const int tid = threadIdx.x;
+    const int plane = p.hp * p.wp;
+    const int taps = TAPS > 0 ? TAPS : p.taps;
 
-    // ---- stage 1: stage the chunk's input maps ----
-    const int nin = mb * hw;
-    if constexpr (PRE == CGP_PRE_MOMENTS) {
-        // division by C mirrors torch's mean (sum, then / C)
-        for (int e = tid; e < nin; e += kBlock) {
-            const int ml = e / hw;
-            const int px = e - ml * hw;
-            unsigned i, j;
-            pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
-            const T* xi = p.in + (size_t)i * p.channels * hw + px;
-            const T* yj = p.in_y + (size_t)j * p.channels * hw + px;
-            T acc = xi[0] * yj[0];
-            for (int c = 1; c < p.channels; ++c) acc += xi[(size_t)c * hw] * yj[(size_t)c * hw];
-            tin[e] = acc / T(p.channels);
-        }
-    } else {
+    // zero the padded planes once: the halo is never written afterwards
+    for (int e = tid; e < p.mpb * plane; e += kBlock) tin[e] = T(0);
+
+    T v[kEMax];
+    // plain map loads go through the prefetch registers; the input moments (first layer
+    // only, small cached image reads) are computed in stage 1 instead
+    const bool prefetch = p.pre != CGP_PRE_MOMENTS;
+    auto load_chunk = [&](long long chunk) {
+        const long long m0 = chunk * p.mpb;
+        const long long rem = p.nmaps - m0;
+        const int nin = (rem < p.mpb ? (int)rem : p.mpb) * hw;
         const T* src = p.in + m0 * hw;
-        constexpr int U = 4;
-        for (int base = tid; base < nin; base += kBlock * U) {
-            T v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = base + u * kBlock;
-                v[u] = e < nin ? src[e] : T(0);
-            }
+        for (int k = 0; k < kEMax; ++k) {
+            const int e = tid + k * kBlock;
+            v[k] = e < nin ? src[e] : T(0);
+        }
+    };
+
+    long long chunk = blockIdx.x;
+    if (prefetch && chunk < p.nchunks) load_chunk(chunk);
+    __syncthreads();   // halo zeroing complete
+    for (; chunk < p.nchunks; chunk += gridDim.x) {
+        const long long m0 = chunk * p.mpb;
+        const long long rem = p.nmaps - m0;
+        const int mb = rem < p.mpb ? (int)rem : p.mpb;
+        const int nin = mb * hw;
+
+        // ---- stage 1: registers -> padded LDS planes ----
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = base + u * kBlock;
-                if (e < nin) {
-                    T x = v[u];
-                    if constexpr (PRE == CGP_PRE_RELU) {
-                        const int ml = e / hw;
-                        const int px = e - ml * hw;
-                        unsigned i, j;
-                        pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
-                        x = relu_pair(x, p.pre_xx, p.pre_yy, i, j, hw, px, p.same, p.diag);
-                    }
-                    tin[e] = x;
-                }
+        for (int k = 0; k < kEMax; ++k) {
+            const int e = tid + k * kBlock;
+            if (prefetch && e < nin) {
+                const unsigned ml = fdiv((unsigned)e, p.dhw);
+                const int px = e - (int)ml * hw;
+                const unsigned r = fdiv((unsigned)px, p.dw);
+                const int c = px - (int)r * p.w;
+                tin[(int)ml * plane + ((int)r + p.plo_r) * p.wp + c + p.plo_c] = v[k];
             }
         }
-    }
-    __syncthreads();
+        // moments, and chunks larger than the prefetch window: direct path
+        for (int e = tid + (prefetch ? kEMax * kBlock : 0); e < nin; e += kBlock) {
+            const unsigned ml = fdiv((unsigned)e, p.dhw);
+            const int px = e - (int)ml * hw;
+            const unsigned r = fdiv((unsigned)px, p.dw);
+            const int c = px - (int)r * p.w;
+            T x;
+            if (p.pre == CGP_PRE_MOMENTS) {
+                unsigned i, j;
+                pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+                const T* xi = p.in + (size_t)i * p.channels * hw + px;
+                const T* yj = p.in_y + (size_t)j * p.channels * hw + px;
+                x = xi[0] * yj[0];
+                for (int cc = 1; cc < p.channels; ++cc)
+                    x += xi[(size_t)cc * hw] * yj[(size_t)cc * hw];
+                x = x / T(p.channels);
+            } else {
+                x = p.in[m0 * hw + e];
+            }
+            tin[(int)ml * plane + ((int)r + p.plo_r) * p.wp + c + p.plo_c] = x;
+        }
+        // PRE ReLU in place on the staged interior (each thread revisits its own writes,
+        // so no barrier is needed before it)
+        if (p.pre == CGP_PRE_RELU) {
+            for (int e = tid; e < nin; e += kBlock) {
+                const unsigned ml = fdiv((unsigned)e, p.dhw);
+                const int px = e - (int)ml * hw;
+                const unsigned r = fdiv((unsigned)px, p.dw);
+                const int c = px - (int)r * p.w;
+                unsigned i, j;
+                pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+                T* slot = tin + (int)ml * plane + ((int)r + p.plo_r) * p.wp + c + p.plo_c;
+                *slot = relu_pair(*slot, p.pre_xx, p.pre_yy, i, j, hw, px, p.same, p.diag,
+                                  p.exact);
+            }
+        }
+        lds_barrier();
 
-    // ---- stage 2: row sums over the horizontal taps ----
-    const int nhs = mb * p.h * p.wo;
-    for (int e = tid; e < nhs; e += kBlock) {
-        const int rr = e / p.wo;            // ml * h + r
-        const int ow = e - rr * p.wo;
-        const T* row = tin + rr * p.w;
-        const int c0 = ow * p.stride + p.off;
-        T acc = T(0);
-        for (int t = 0; t < p.taps; ++t) {
-            const int c = c0 + t * p.dil;
-            if ((unsigned)c < (unsigned)p.w) acc += row[c];
-        }
-        ths[e] = acc;
-    }
-    __syncthreads();
+        // the next chunk's HBM reads fly while this one is computed
+        if (prefetch && chunk + gridDim.x < p.nchunks) load_chunk(chunk + gridDim.x);
 
-    // ---- stage 3: column sums, affine, fused epilogue, store ----
-    const int nout = mb * howo;
-    T* dst = p.out + m0 * howo;
-    const T* add = ADD ? p.addend + m0 * howo : nullptr;
-    for (int e = tid; e < nout; e += kBlock) {
-        const int ml = e / howo;
-        const int q = e - ml * howo;
-        const int oh = q / p.wo;
-        const int ow = q - oh * p.wo;
-        const T* col = ths + ml * p.h * p.wo + ow;
-        const int r0 = oh * p.stride + p.off;
-        T acc = T(0);
-        for (int t = 0; t < p.taps; ++t) {
-            const int r = r0 + t * p.dil;
-            if ((unsigned)r < (unsigned)p.h) acc += col[r * p.wo];
+        // ---- stage 2: row sums over the horizontal taps (every padded row) ----
+        const int nhs = mb * p.hp * p.wo;
+        for (int e = tid; e < nhs; e += kBlock) {
+            const unsigned rowi = fdiv((unsigned)e, p.dwo);        // ml * hp + rp
+            const int ow = e - (int)rowi * p.wo;
+            const T* src = tin + (int)rowi * p.wp + ow * p.stride + p.c0;
+            T acc = src[0];
+#pragma unroll
+            for (int t = 1; t < (TAPS > 0 ? TAPS : 1); ++t) acc += src[t * p.dil];
+            if (TAPS == 0)
+                for (int t = 1; t < taps; ++t) acc += src[t * p.dil];
+            ths[e] = acc;
         }
-        T v = p.weight * acc + p.bias;
-        if constexpr (POST == CGP_POST_RELU) {
-            unsigned i, j;
-            pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
-            v = relu_pair(v, p.post_xx, p.post_yy, i, j, howo, q, p.same, p.diag);
+        lds_barrier();
+
+        // ---- stage 3: column sums, affine, fused epilogue, store ----
+        const int nout = mb * howo;
+        T* dst = p.out + m0 * howo;
+        const T* add = p.add ? p.addend + m0 * howo : nullptr;
+        for (int e = tid; e < nout; e += kBlock) {
+            const unsigned ml = fdiv((unsigned)e, p.dhowo);
+            const int q = e - (int)ml * howo;
+            const unsigned oh = fdiv((unsigned)q, p.dwo);
+            const int ow = q - (int)oh * p.wo;
+            const T* col = ths + ((int)ml * p.hp + (int)oh * p.stride + p.r0) * p.wo + ow;
+            const int cs = p.dil * p.wo;
+            T acc = col[0];
+#pragma unroll
+            for (int t = 1; t < (TAPS > 0 ? TAPS : 1); ++t) acc += col[t * cs];
+            if (TAPS == 0)
+                for (int t = 1; t < taps; ++t) acc += col[t * cs];
+            T val = p.weight * acc + p.bias;
+            if (p.post == CGP_POST_RELU) {
+                unsigned i, j;
+                pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+                val = relu_pair(val, p.post_xx, p.post_yy, i, j, howo, q, p.same, p.diag,
+                                p.exact);
+            }
+            if (p.add) val = val + add[e];
+            dst[e] = val;
         }
-        if constexpr (ADD) v = v + add[e];
-        dst[e] = v;
     }
 }
 
 // ----------------------------------------------------------------------------------
-// standalone ReLU on pair maps (+ optional addend), chunked like the conv
+// Conv2d covariance stencil for the geometries the configs use (compile-time shapes).
+//
+// Same chunked algorithm as conv_cov_kernel, with every map dimension a compile-time
+// constant, so index math folds to shifts/multiply-highs, the tap loops unroll into
+// ds_read_b64 with immediate offsets, and the parameter block stays small (no SGPR
+// spills).  Memory pipeline per chunk (one chunk = MB whole maps):
+//   top      wait for this chunk's input DMA; issue its variance/addend loads (registers)
+//   stage 1  input staging -> zero-haloed padded planes (+ PRE ReLU / input moments)
+//   DMA      next chunk's input maps HBM -> LDS staging (global_load_lds, fixed count
+//            per wave, branch-free), in flight during stages 2-3
+//   stage 2  row sums, one output per item
+//   stage 3  column sums, R3 output rows per item; ·w + b, POST ReLU, + addend, store
+// ----------------------------------------------------------------------------------
+template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_>
+struct Geo {
+    static constexpr int H = H_, W = W_, HO = HO_, WO = WO_, TAPS = TAPS_, S = S_, OFF = OFF_;
+    static constexpr int HW = H * W, HOWO = HO * WO;
+    static constexpr int PLO = OFF < 0 ? -OFF : 0;
+    static constexpr int R3 = HO >= 8 ? 4 : (HO >= 2 ? 2 : 1);   // rows per stage-3 item
+    static constexpr int HOS = (HO + R3 - 1) / R3 * R3;
+    static constexpr int LASTC = (WO - 1) * S + OFF + TAPS - 1;
+    static constexpr int LASTR = (HOS - 1) * S + OFF + TAPS - 1;
+    static constexpr int WP = W + PLO + (LASTC > W - 1 ? LASTC - (W - 1) : 0);
+    static constexpr int HP = H + PLO + (LASTR > H - 1 ? LASTR - (H - 1) : 0);
+    static constexpr int C0 = OFF + PLO, R0 = OFF + PLO;
+    static constexpr int PL = HP * WP;
+    static constexpr int WIN = (R3 - 1) * S + TAPS;               // stage-3 register window
+};
+
+constexpr int cround(int n, int a) { return (n + a - 1) / a * a; }
+
+template <typename T, class G>
+struct GeoLayout {
+    static constexpr int al = 16 / (int)sizeof(T);
+    static constexpr int PAD = 1024 / (int)sizeof(T);   // DMA tail slack after a staging buffer
+    static constexpr int lds_elems(int mb) {
+        return 2 * (cround(mb * G::HW, al) + PAD) + cround(mb * G::PL, al) +
+               cround(mb * G::HP * G::WO, al);
+    }
+    static constexpr int pick_mb() {
+        int mb = kChunkElems / G::HW;
+        if (mb < 1) mb = 1;
+        if (mb > 16) mb = 16;
+        while (mb > 1 && lds_elems(mb) * (int)sizeof(T) > 32 * 1024) --mb;
+        return mb;
+    }
+    static constexpr int MB = pick_mb();
+    static constexpr int IN_STRIDE = cround(MB * G::HW, al) + PAD;   // two input buffers
+    static constexpr int L_PLANE = 2 * IN_STRIDE;
+    static constexpr int L_HS = L_PLANE + cround(MB * G::PL, al);
+    static constexpr int ELEMS = L_HS + cround(MB * G::HP * G::WO, al);
+    static constexpr int IN_BYTES = MB * G::HW * (int)sizeof(T);
+    static constexpr int DMA16 = (IN_BYTES % 16) == 0 && (G::HW * (int)sizeof(T)) % 16 == 0;
+    static constexpr int PIECE = DMA16 ? 1024 : 256;
+    static constexpr int PIECES = (IN_BYTES + PIECE - 1) / PIECE;
+    static constexpr int PW = (PIECES + kBlock / 64 - 1) / (kBlock / 64);   // per wave
+    static constexpr int N3 = MB * (G::HOS / G::R3) * G::WO;
+    static constexpr int I3 = (N3 + kBlock - 1) / kBlock;
+};
+
+template <typename T>
+struct GeoP {
+    const T* in;
+    const T* in_y;
+    T* out;
+    const T* addend;
+    const T* pre_xx;
+    const T* pre_yy;
+    const T* post_xx;
+    const T* post_yy;
+    long long nmaps, nchunks;
+    FastDiv n2;
+    int channels, pre, post, add, same, diag;
+    T weight, bias;
+};
+
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// The chunk's input maps -> LDS staging by LDS-DMA: exactly PW instructions per wave with
+// all 64 lanes active (sources clamped into the chunk, tails land in the pad), so the
+// compiler's vmcnt bookkeeping for loads issued before it stays exact.
+template <typename T, class G>
+__device__ __forceinline__ void geo_dma_input(const GeoP<T>& p, long long chunk,
+                                              unsigned char* smem, int wave, int lane) {
+    // smem: this buffer's base
+    using L = GeoLayout<T, G>;
+    const long long m0 = chunk * L::MB;
+    const long long rem = p.nmaps - m0;
+    const int nbytes = (rem < L::MB ? (int)rem : L::MB) * G::HW * (int)sizeof(T);
+    const char* src = reinterpret_cast<const char*>(p.in + m0 * G::HW);
+#pragma unroll
+    for (int k = 0; k < L::PW; ++k) {
+        int pc = wave * L::PW + k;
+        if (pc >= L::PIECES) pc = L::PIECES - 1;                   // duplicate, harmless
+        int o = pc * L::PIECE + lane * (L::PIECE / 64);
+        if (o > nbytes - L::PIECE / 64) o = nbytes - L::PIECE / 64;   // clamp the tail
+        unsigned char* dst = smem + (size_t)pc * L::PIECE;
+        if constexpr (L::DMA16)
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + o), (lptr_t)dst, 16, 0, 0);
+        else
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + o), (lptr_t)dst, 4, 0, 0);
+    }
+}
+
+template <typename T, class G, int PRE, bool POST, bool ADD>
+__global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
+    using L = GeoLayout<T, G>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
+    T* plane = lds + L::L_PLANE;
+    T* hs = lds + L::L_HS;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr bool moments = PRE == CGP_PRE_MOMENTS;
+    auto inbuf = [&](int b) { return smem + (size_t)b * L::IN_STRIDE * sizeof(T); };
+
+    for (int e = tid; e < L::MB * G::PL; e += kBlock) plane[e] = T(0);   // halo: zero forever
+    // input DMA runs two chunks ahead: chunk k's maps land in buffer k & 1
+    long long chunk = blockIdx.x;
+    if constexpr (!moments) {
+        if (chunk < p.nchunks) {
+            const long long c1 = chunk + gridDim.x;
+            geo_dma_input<T, G>(p, chunk, inbuf(0), wave, lane);
+            geo_dma_input<T, G>(p, c1 < p.nchunks ? c1 : chunk, inbuf(1), wave, lane);
+        }
+    }
+
+    for (int buf = 0; chunk < p.nchunks; chunk += gridDim.x, buf ^= 1) {
+        const long long m0 = chunk * L::MB;
+        const long long rem = p.nmaps - m0;
+        const int mb = rem < L::MB ? (int)rem : L::MB;
+        const T* sin = reinterpret_cast<const T*>(inbuf(buf));
+        // this chunk's DMA is older than the last PW VM ops (the next chunk's DMA)
+        if constexpr (moments)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::PW) : "memory");
+        lds_barrier();
+
+        // variance / addend values this thread's stage-3 outputs need (loaded now, used
+        // after stage 2; the compiler counts the DMA issued in between)
+        T vx[L::I3][G::R3], vy[L::I3][G::R3], ad[L::I3][G::R3];
+        unsigned pi[L::I3], pj[L::I3];
+#pragma unroll
+        for (int k = 0; k < L::I3; ++k) {
+            int e = tid + k * kBlock;
+            if (e >= mb * (G::HOS / G::R3) * G::WO) e = 0;             // clamp: valid address
+            const int ow = e % G::WO;
+            const int rr = e / G::WO;
+            const int ml = rr / (G::HOS / G::R3);
+            const int oh0 = (rr - ml * (G::HOS / G::R3)) * G::R3;
+            unsigned i = 0, j = 0;
+            pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+            pi[k] = i;
+            pj[k] = j;
+#pragma unroll
+            for (int o = 0; o < G::R3; ++o) {
+                const int oh = oh0 + o < G::HO ? oh0 + o : G::HO - 1;
+                const int q = oh * G::WO + ow;
+                if constexpr (POST) {
+                    vx[k][o] = p.post_xx[(size_t)i * G::HOWO + q];
+                    vy[k][o] = p.post_yy[(size_t)j * G::HOWO + q];
+                }
+                if constexpr (ADD) ad[k][o] = p.addend[(m0 + ml) * G::HOWO + q];
+            }
+        }
+
+        // ---- stage 1: staging -> padded planes (+ PRE ReLU, or the input moments) ----
+        for (int e = tid; e < mb * G::HW; e += kBlock) {
+            const int ml = e / G::HW;
+            const int px = e - ml * G::HW;
+            const int r = px / G::W;
+            const int c = px - r * G::W;
+            T x;
+            if constexpr (moments) {
+                unsigned i, j;
+                pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+                const T* xi = p.in + (size_t)i * p.channels * G::HW + px;
+                const T* yj = p.in_y + (size_t)j * p.channels * G::HW + px;
+                x = xi[0] * yj[0];
+                for (int cc = 1; cc < p.channels; ++cc)
+                    x += xi[(size_t)cc * G::HW] * yj[(size_t)cc * G::HW];
+                x = x / T(p.channels);
+            } else {
+                x = sin[e];
+                if constexpr (PRE == CGP_PRE_RELU) {
+                    unsigned i, j;
+                    pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+                    x = relu_pair(x, p.pre_xx, p.pre_yy, i, j, G::HW, px, p.same, p.diag, 0);
+                }
+            }
+            plane[ml * G::PL + (r + G::PLO) * G::WP + c + G::PLO] = x;
+        }
+        lds_barrier();
+
+        // ---- stage 2: row sums (every padded row), one output per item ----
+        for (int e = tid; e < mb * G::HP * G::WO; e += kBlock) {
+            const int rowi = e / G::WO;                           // ml * HP + rp
+            const int ow = e - rowi * G::WO;
+            const T* src = plane + rowi * G::WP + ow * G::S + G::C0;
+            T acc = src[0];
+#pragma unroll
+            for (int t = 1; t < G::TAPS; ++t) acc += src[t];
+            hs[e] = acc;
+        }
+        lds_barrier();
+
+        // ---- stage 3: column sums over R3 rows per item, epilogue, store ----
+        T* out = p.out + m0 * G::HOWO;
+#pragma unroll
+        for (int k = 0; k < L::I3; ++k) {
+            const int e = tid + k * kBlock;
+            if (e < mb * (G::HOS / G::R3) * G::WO) {
+                const int ow = e % G::WO;
+                const int rr = e / G::WO;
+                const int ml = rr / (G::HOS / G::R3);
+                const int oh0 = (rr - ml * (G::HOS / G::R3)) * G::R3;
+                const T* src = hs + (ml * G::HP + oh0 * G::S + G::R0) * G::WO + ow;
+                T win[G::WIN];
+#pragma unroll
+                for (int t = 0; t < G::WIN; ++t) win[t] = src[t * G::WO];
+                T res[G::R3];
+#pragma unroll
+                for (int o = 0; o < G::R3; ++o) {
+                    T acc = win[o * G::S];
+#pragma unroll
+                    for (int t = 1; t < G::TAPS; ++t) acc += win[o * G::S + t];
+                    res[o] = p.weight * acc + p.bias;
+                }
+                if constexpr (POST) {
+                    const bool ovr = p.same && (p.diag || pi[k] == pj[k]);
+#pragma unroll
+                    for (int o = 0; o < G::R3; ++o) {
+                        const T r = relu_fast(res[o], vx[k][o], vy[k][o]);
+                        res[o] = ovr ? vx[k][o] / T(2) : r;
+                    }
+                }
+                // materialise every result before the first (predicated) store: otherwise
+                // hipcc sinks each output's math into its store block and re-waits vmcnt(0)
+                // per block, serialising on the stores just issued
+#pragma unroll
+                for (int o = 0; o < G::R3; ++o) {
+                    if constexpr (ADD) res[o] = res[o] + ad[k][o];
+                    asm volatile("" ::"v"(res[o]));
+                }
+#pragma unroll
+                for (int o = 0; o < G::R3; ++o) {
+                    if (oh0 + o < G::HO) out[ml * G::HOWO + (oh0 + o) * G::WO + ow] = res[o];
+                }
+            }
+        }
+        // buffer `buf` was consumed in stage 1: fetch chunk k+2 into it (unconditional —
+        // past the end it re-fetches this chunk — so every path issues exactly PW ops)
+        if constexpr (!moments) {
+            const long long nxt = chunk + 2 * (long long)gridDim.x;
+            geo_dma_input<T, G>(p, nxt < p.nchunks ? nxt : chunk, inbuf(buf), wave, lane);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// the geometries of configs/*.py (taps, stride, offset as Conv2d lowers them)
+#define CGP_GEOMETRIES(X)            \
+    X(28, 28, 28, 28, 7, 1, -3)      \
+    X(28, 28, 28, 28, 1, 1, 0)       \
+    X(32, 32, 32, 32, 1, 1, 0)       \
+    X(28, 28, 28, 28, 4, 1, -1)      \
+    X(28, 28, 28, 28, 3, 1, -1)      \
+    X(28, 28, 14, 14, 3, 2, -1)      \
+    X(28, 28, 14, 14, 1, 2, 0)       \
+    X(14, 14, 14, 14, 3, 1, -1)      \
+    X(14, 14, 7, 7, 3, 2, -1)        \
+    X(14, 14, 7, 7, 1, 2, 0)         \
+    X(7, 7, 7, 7, 3, 1, -1)          \
+    X(32, 32, 32, 32, 3, 1, -1)      \
+    X(32, 32, 16, 16, 3, 2, -1)      \
+    X(32, 32, 16, 16, 1, 2, 0)       \
+    X(16, 16, 16, 16, 3, 1, -1)      \
+    X(16, 16, 8, 8, 3, 2, -1)        \
+    X(16, 16, 8, 8, 1, 2, 0)         \
+    X(8, 8, 8, 8, 3, 1, -1)
+
+// ----------------------------------------------------------------------------------
+// standalone ReLU on pair maps (+ optional addend), one chunk of maps per workgroup
 // ----------------------------------------------------------------------------------
 template <typename T>
 struct ReluP {
@@ -258,8 +679,8 @@ struct ReluP {
     const T* xx;
     const T* yy;
     long long nmaps;
-    unsigned n2;
-    int hw, same, diag, mpb;
+    FastDiv n2, dhw;
+    int hw, same, diag, exact, mpb;
 };
 
 template <typename T, bool ADD>
@@ -271,26 +692,23 @@ __global__ __launch_bounds__(kBlock) void relu_pair_kernel(const ReluP<T> p) {
     const T* src = p.xy + m0 * p.hw;
     T* dst = p.out + m0 * p.hw;
     const T* add = ADD ? p.addend + m0 * p.hw : nullptr;
-    constexpr int U = 4;
-    for (int base = threadIdx.x; base < n; base += kBlock * U) {
-        T v[U];
+    T v[kEMax];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = base + u * kBlock;
-            v[u] = e < n ? src[e] : T(0);
-        }
+    for (int k = 0; k < kEMax; ++k) {
+        const int e = threadIdx.x + k * kBlock;
+        v[k] = e < n ? src[e] : T(0);
+    }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = base + u * kBlock;
-            if (e < n) {
-                const int ml = e / p.hw;
-                const int px = e - ml * p.hw;
-                unsigned i, j;
-                pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
-                T r = relu_pair(v[u], p.xx, p.yy, i, j, p.hw, px, p.same, p.diag);
-                if constexpr (ADD) r = r + add[e];
-                dst[e] = r;
-            }
+    for (int k = 0; k < kEMax; ++k) {
+        const int e = threadIdx.x + k * kBlock;
+        if (e < n) {
+            const unsigned ml = fdiv((unsigned)e, p.dhw);
+            const int px = e - (int)ml * p.hw;
+            unsigned i, j;
+            pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
+            T r = relu_pair(v[k], p.xx, p.yy, i, j, p.hw, px, p.same, p.diag, p.exact);
+            if constexpr (ADD) r = r + add[e];
+            dst[e] = r;
         }
     }
 }
@@ -317,8 +735,9 @@ __global__ __launch_bounds__(kBlock) void var_relu_kernel(const T* __restrict__ 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void moments_xy_kernel(const T* __restrict__ x,
                                                             const T* __restrict__ y,
-                                                            long long nmaps, unsigned n2,
-                                                            int c, int hw, int diag, int mpb,
+                                                            long long nmaps, FastDiv n2,
+                                                            FastDiv dhw, int c, int hw,
+                                                            int diag, int mpb,
                                                             T* __restrict__ xy) {
     const long long m0 = (long long)blockIdx.x * mpb;
     long long rem = nmaps - m0;
@@ -326,8 +745,8 @@ __global__ __launch_bounds__(kBlock) void moments_xy_kernel(const T* __restrict_
     const int n = mb * hw;
     T* dst = xy + m0 * hw;
     for (int e = threadIdx.x; e < n; e += kBlock) {
-        const int ml = e / hw;
-        const int px = e - ml * hw;
+        const unsigned ml = fdiv((unsigned)e, dhw);
+        const int px = e - (int)ml * hw;
         unsigned i, j;
         pair_of((unsigned)(m0 + ml), n2, diag, i, j);
         const T* xi = x + (size_t)i * c * hw + px;
@@ -432,12 +851,29 @@ inline int maps_per_chunk(int hw, int requested) {
     return m < 1 ? 1 : m;
 }
 
+// compute units of the current device (cached; launch geometry of persistent kernels)
+int device_cus() {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+        n = 256;
+    cache[dev] = n;
+    return n;
+}
+
 int conv_out_check(const cgp_conv_args* a) {
     if (!a) return fail(CGP_EINVAL, "conv: args is NULL");
     if (!a->in || !a->out) return fail(CGP_EINVAL, "conv: in/out is NULL");
     if (a->nmaps <= 0 || a->nmaps >= (1LL << 31))
         return fail(CGP_EINVAL, "conv: nmaps=%lld out of range", (long long)a->nmaps);
-    if (a->h <= 0 || a->w <= 0 || a->ho <= 0 || a->wo <= 0)
+    if (a->h <= 0 || a->w <= 0 || a->ho <= 0 || a->wo <= 0 || (long long)a->h * a->w >= (1 << 24))
         return fail(CGP_EINVAL, "conv: bad spatial sizes %dx%d -> %dx%d", a->h, a->w, a->ho,
                     a->wo);
     if (a->taps <= 0 || a->stride <= 0 || a->dilation <= 0)
@@ -476,33 +912,118 @@ int conv_out_check(const cgp_conv_args* a) {
     return CGP_OK;
 }
 
-template <typename T, int PRE, int POST, bool ADD>
-void launch_conv(const ConvP<T>& p, unsigned grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((conv_cov_kernel<T, PRE, POST, ADD>), dim3(grid), dim3(kBlock), lds, s,
+// persistent grid: exactly as many workgroups as can be resident at once (registers and
+// LDS both counted by the occupancy query), so no workgroup starts late
+template <typename T, int TAPS>
+int launch_conv(const ConvP<T>& p, size_t lds, hipStream_t s) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_cov_kernel<T, TAPS>, kBlock,
+                                                     lds) != hipSuccess || per_cu < 1) {
+        (void)hipGetLastError();
+        per_cu = 1;
+    }
+    const long long grid = std::min<long long>(p.nchunks, (long long)per_cu * device_cus());
+    hipLaunchKernelGGL((conv_cov_kernel<T, TAPS>), dim3((unsigned)grid), dim3(kBlock), lds, s,
                        p);
+    return check_launch("conv_cov_kernel");
 }
 
-template <typename T, int PRE, int POST>
-void launch_conv_add(const ConvP<T>& p, bool add, unsigned grid, size_t lds, hipStream_t s) {
-    if (add)
-        launch_conv<T, PRE, POST, true>(p, grid, lds, s);
-    else
-        launch_conv<T, PRE, POST, false>(p, grid, lds, s);
+template <typename T, class G, int PRE, bool POST, bool ADD>
+int launch_geo(const cgp_conv_args* a, hipStream_t s) {
+    using L = GeoLayout<T, G>;
+    GeoP<T> p;
+    p.in = static_cast<const T*>(a->in);
+    p.in_y = static_cast<const T*>(a->in_y);
+    p.out = static_cast<T*>(a->out);
+    p.addend = static_cast<const T*>(a->addend);
+    p.pre_xx = static_cast<const T*>(a->pre_xx);
+    p.pre_yy = static_cast<const T*>(a->pre_yy);
+    p.post_xx = static_cast<const T*>(a->post_xx);
+    p.post_yy = static_cast<const T*>(a->post_yy);
+    p.nmaps = a->nmaps;
+    p.nchunks = (a->nmaps + L::MB - 1) / L::MB;
+    p.n2 = make_fastdiv((unsigned)(a->n2 > 0 ? a->n2 : 1));
+    p.channels = a->channels;
+    p.pre = a->pre;
+    p.post = a->post;
+    p.add = a->addend != nullptr;
+    p.same = a->same;
+    p.diag = a->diag;
+    p.weight = (T)a->weight;
+    p.bias = (T)a->bias;
+    const size_t lds = (size_t)L::ELEMS * sizeof(T);
+    auto kern = conv_geo_kernel<T, G, PRE, POST, ADD>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, lds) != hipSuccess ||
+        per_cu < 1) {
+        (void)hipGetLastError();
+        per_cu = 1;
+    }
+    const long long grid = std::min<long long>(p.nchunks, (long long)per_cu * device_cus());
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, s, p);
+    return check_launch("conv_geo_kernel");
+}
+
+// the fused (pre, post, add) combinations the program fuser emits
+template <typename T, class G>
+int launch_geo_mode(const cgp_conv_args* a, hipStream_t s, bool* handled) {
+    const bool post = a->post == CGP_POST_RELU, add = a->addend != nullptr;
+    *handled = true;
+    switch (a->pre * 4 + post * 2 + add) {
+        case 0: return launch_geo<T, G, CGP_PRE_NONE, false, false>(a, s);
+        case 2: return launch_geo<T, G, CGP_PRE_NONE, true, false>(a, s);
+        case 1: return launch_geo<T, G, CGP_PRE_NONE, false, true>(a, s);
+        case 3: return launch_geo<T, G, CGP_PRE_NONE, true, true>(a, s);
+        case 6: return launch_geo<T, G, CGP_PRE_RELU, true, false>(a, s);
+        case 10: return launch_geo<T, G, CGP_PRE_MOMENTS, true, false>(a, s);
+        case 8: return launch_geo<T, G, CGP_PRE_MOMENTS, false, false>(a, s);
+    }
+    *handled = false;
+    return CGP_OK;
+}
+
+// compile-time-geometry launch; *handled = false when the shape/mode is not in the table
+template <typename T>
+int conv_geo_impl(const cgp_conv_args* a, void* stream, bool* handled) {
+    *handled = false;
+    if (a->dilation != 1 || a->maps_per_block != 0 || (a->flags & CGP_FLAG_EXACT_RELU))
+        return CGP_OK;
+    hipStream_t s = as_stream(stream);
+#define CGP_GEO_CASE(h_, w_, ho_, wo_, k_, s_, o_)                                         \
+    if (a->h == h_ && a->w == w_ && a->ho == ho_ && a->wo == wo_ && a->taps == k_ &&       \
+        a->stride == s_ && a->offset == o_)                                               \
+        return launch_geo_mode<T, Geo<h_, w_, ho_, wo_, k_, s_, o_>>(a, s, handled);
+    CGP_GEOMETRIES(CGP_GEO_CASE)
+#undef CGP_GEO_CASE
+    return CGP_OK;
 }
 
 template <typename T>
 int conv_impl(const cgp_conv_args* a, void* stream) {
     int rc = conv_out_check(a);
     if (rc) return rc;
+    if (!(a->flags & CGP_FLAG_GENERIC_CONV)) {
+        bool handled = false;
+        rc = conv_geo_impl<T>(a, stream, &handled);
+        if (rc || handled) return rc;
+    }
     const int hw = a->h * a->w;
+    // zero halo around each staged map: every tap read lands inside the padded plane
+    const int span = (a->taps - 1) * a->dilation;
+    const int plo = a->offset < 0 ? -a->offset : 0;
+    const int phi_r = std::max(0, (a->ho - 1) * a->stride + a->offset + span - (a->h - 1));
+    const int phi_c = std::max(0, (a->wo - 1) * a->stride + a->offset + span - (a->w - 1));
+    const int hp = a->h + plo + phi_r, wp = a->w + plo + phi_c;
     int mpb = maps_per_chunk(hw, a->maps_per_block);
     auto lds_of = [&](int m) {
-        const size_t in_elems = ((size_t)m * hw + 1) & ~(size_t)1;   // keep 16-B alignment
-        return (in_elems + (size_t)m * a->h * a->wo) * sizeof(T);
+        const size_t in_elems = ((size_t)m * hp * wp + 1) & ~(size_t)1;  // 16-B aligned
+        return (in_elems + (size_t)m * hp * a->wo) * sizeof(T);
     };
     while (mpb > 1 && lds_of(mpb) > (size_t)kMaxLds) --mpb;
     if (lds_of(mpb) > (size_t)kMaxLds)
         return fail(CGP_EINVAL, "conv: one %dx%d map does not fit the LDS budget", a->h, a->w);
+    if ((long long)mpb * hw > kChunkElems && (long long)mpb * hw >= (1LL << 30))
+        return fail(CGP_EINVAL, "conv: chunk too large");
     ConvP<T> p;
     p.in = static_cast<const T*>(a->in);
     p.in_y = static_cast<const T*>(a->in_y);
@@ -513,45 +1034,47 @@ int conv_impl(const cgp_conv_args* a, void* stream) {
     p.post_xx = static_cast<const T*>(a->post_xx);
     p.post_yy = static_cast<const T*>(a->post_yy);
     p.nmaps = a->nmaps;
-    p.n2 = (unsigned)(a->n2 > 0 ? a->n2 : 1);
+    p.nchunks = (a->nmaps + mpb - 1) / mpb;
+    p.n2 = make_fastdiv((unsigned)(a->n2 > 0 ? a->n2 : 1));
+    p.dw = make_fastdiv((unsigned)a->w);
+    p.dhw = make_fastdiv((unsigned)hw);
+    p.dwo = make_fastdiv((unsigned)a->wo);
+    p.dhowo = make_fastdiv((unsigned)(a->ho * a->wo));
     p.h = a->h;
     p.w = a->w;
     p.ho = a->ho;
     p.wo = a->wo;
+    p.hp = hp;
+    p.wp = wp;
+    p.plo_r = plo;
+    p.plo_c = plo;
+    p.c0 = a->offset + plo;
+    p.r0 = a->offset + plo;
     p.taps = a->taps;
-    p.off = a->offset;
     p.stride = a->stride;
     p.dil = a->dilation;
     p.channels = a->channels;
+    p.pre = a->pre;
+    p.post = a->post;
+    p.add = a->addend != nullptr;
     p.same = a->same;
     p.diag = a->diag;
+    p.exact = (a->flags & CGP_FLAG_EXACT_RELU) != 0;
     p.mpb = mpb;
-    p.hs_offset = (int)(((size_t)mpb * hw + 1) & ~(size_t)1);
+    p.hs_offset = (int)(((size_t)mpb * hp * wp + 1) & ~(size_t)1);
     p.weight = (T)a->weight;
     p.bias = (T)a->bias;
-    const long long blocks = (a->nmaps + mpb - 1) / mpb;
-    if (blocks > 0x7fffffffLL) return fail(CGP_EINVAL, "conv: grid too large");
-    const unsigned grid = (unsigned)blocks;
     const size_t lds = lds_of(mpb);
-    const bool add = a->addend != nullptr;
     hipStream_t s = as_stream(stream);
-    switch (a->pre * 2 + a->post) {
-        case CGP_PRE_NONE * 2 + CGP_POST_NONE:
-            launch_conv_add<T, CGP_PRE_NONE, CGP_POST_NONE>(p, add, grid, lds, s); break;
-        case CGP_PRE_NONE * 2 + CGP_POST_RELU:
-            launch_conv_add<T, CGP_PRE_NONE, CGP_POST_RELU>(p, add, grid, lds, s); break;
-        case CGP_PRE_RELU * 2 + CGP_POST_NONE:
-            launch_conv_add<T, CGP_PRE_RELU, CGP_POST_NONE>(p, add, grid, lds, s); break;
-        case CGP_PRE_RELU * 2 + CGP_POST_RELU:
-            launch_conv_add<T, CGP_PRE_RELU, CGP_POST_RELU>(p, add, grid, lds, s); break;
-        case CGP_PRE_MOMENTS * 2 + CGP_POST_NONE:
-            launch_conv_add<T, CGP_PRE_MOMENTS, CGP_POST_NONE>(p, add, grid, lds, s); break;
-        case CGP_PRE_MOMENTS * 2 + CGP_POST_RELU:
-            launch_conv_add<T, CGP_PRE_MOMENTS, CGP_POST_RELU>(p, add, grid, lds, s); break;
-        default:
-            return fail(CGP_EINVAL, "conv: bad pre/post");
+    switch (a->taps) {
+        case 1: return launch_conv<T, 1>(p, lds, s);
+        case 2: return launch_conv<T, 2>(p, lds, s);
+        case 3: return launch_conv<T, 3>(p, lds, s);
+        case 4: return launch_conv<T, 4>(p, lds, s);
+        case 5: return launch_conv<T, 5>(p, lds, s);
+        case 7: return launch_conv<T, 7>(p, lds, s);
+        default: return launch_conv<T, 0>(p, lds, s);
     }
-    return check_launch("conv_cov_kernel");
 }
 
 template <typename T>
@@ -571,11 +1094,15 @@ int relu_impl(const cgp_relu_args* a, void* stream) {
     p.xx = static_cast<const T*>(a->xx);
     p.yy = static_cast<const T*>(a->yy);
     p.nmaps = a->nmaps;
-    p.n2 = (unsigned)a->n2;
+    p.n2 = make_fastdiv((unsigned)a->n2);
+    p.dhw = make_fastdiv((unsigned)a->hw);
     p.hw = a->hw;
     p.same = a->same;
     p.diag = a->diag;
-    p.mpb = maps_per_chunk(a->hw, 0);
+    p.exact = (a->flags & CGP_FLAG_EXACT_RELU) != 0;
+    // one chunk of whole maps per workgroup, at most kEMax elements per thread
+    p.mpb = std::max(1, kChunkElems / a->hw);
+    if (a->hw > kChunkElems) return fail(CGP_EINVAL, "relu: map of %d pixels too large", a->hw);
     const long long blocks = (a->nmaps + p.mpb - 1) / p.mpb;
     hipStream_t s = as_stream(stream);
     if (a->addend)
@@ -610,7 +1137,8 @@ int moments_xy_impl(const T* x, const T* y, int64_t n1, int64_t n2, int32_t c, i
     const int mpb = maps_per_chunk(hw, 0);
     const long long blocks = (nmaps + mpb - 1) / mpb;
     hipLaunchKernelGGL((moments_xy_kernel<T>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       as_stream(stream), x, y, nmaps, (unsigned)n2, c, hw, diag, mpb, xy);
+                       as_stream(stream), x, y, nmaps, make_fastdiv((unsigned)n2),
+                       make_fastdiv((unsigned)hw), c, hw, diag, mpb, xy);
     return check_launch("moments_xy_kernel");
 }
 
@@ -673,6 +1201,26 @@ int cgp_abi_version(void) { return CGP_ABI_VERSION; }
 const char* cgp_last_error(void) { return g_last_error.c_str(); }
 size_t cgp_conv_args_size(void) { return sizeof(cgp_conv_args); }
 size_t cgp_relu_args_size(void) { return sizeof(cgp_relu_args); }
+
+int cgp_selftest(void) {
+    // FastDiv against exact division: every divisor the kernels use, edge numerators
+    const unsigned divs[] = {1, 2, 3, 5, 7, 8, 14, 28, 49, 196, 784, 1000, 1024, 4095, 4096,
+                             40000, 65535, 1000003u, 0x7fffffffu};
+    unsigned long long seed = 0x9e3779b97f4a7c15ull;
+    for (unsigned d : divs) {
+        const FastDiv f = make_fastdiv(d);
+        const unsigned edge[] = {0u, 1u, d - 1, d, d + 1, 2 * d - 1, 0x7ffffffeu, 0x7fffffffu};
+        for (unsigned n : edge)
+            if (n < 0x80000000u && fdiv(n, f) != n / d)
+                return fail(CGP_EINVAL, "fastdiv %u / %u", n, d);
+        for (int k = 0; k < 200000; ++k) {
+            seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+            const unsigned n = (unsigned)(seed >> 33) & 0x7fffffffu;
+            if (fdiv(n, f) != n / d) return fail(CGP_EINVAL, "fastdiv %u / %u", n, d);
+        }
+    }
+    return CGP_OK;
+}
 
 int cgp_device_count(void) {
     int n = 0;

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 1
+#define CGP_ABI_VERSION 2
 
 /* error codes */
 #define CGP_OK 0
@@ -48,6 +48,13 @@ extern "C" {
 #define CGP_POST_NONE 0
 #define CGP_POST_RELU 1    /* apply the ReLU covariance map to the conv output */
 
+/* cgp_conv_args.flags / cgp_relu_args.flags */
+#define CGP_FLAG_EXACT_RELU 1  /* evaluate the ReLU map op by op like the reference
+                                  (correctly rounded 1/sqrt, sqrt, acos, division);
+                                  default is the closed form max(c,0)/2 + sqrt(t)·x^1.5·P(x)
+                                  of csrc/relu_poly.h, within 1e-14 of the exact map */
+#define CGP_FLAG_GENERIC_CONV 2  /* force the generic conv kernel (tests / A-B timing) */
+
 int cgp_abi_version(void);
 const char* cgp_last_error(void);
 /* sizeof of the argument structs, so an FFI can verify its mirror of the layout */
@@ -55,6 +62,8 @@ size_t cgp_conv_args_size(void);
 size_t cgp_relu_args_size(void);
 /* number of visible HIP devices (0 without a GPU; never fails) */
 int cgp_device_count(void);
+/* host-only self test of the library's integer helpers (no GPU needed); 0 = pass */
+int cgp_selftest(void);
 
 /*
  * Input moments — replaces NNGPKernel.forward's moment step, kernels.py:44-49:
@@ -107,6 +116,8 @@ typedef struct cgp_conv_args {
     int32_t pre, post;
     int32_t same, diag;   /* KernelPatch.same / .diag (kernel_patch.py:4-30) */
     int32_t maps_per_block; /* 0 = library default */
+    int32_t flags;          /* CGP_FLAG_* */
+    int32_t reserved;
     double weight, bias;
 } cgp_conv_args;
 int cgp_conv_f64(const cgp_conv_args* args, void* stream);
@@ -126,7 +137,7 @@ typedef struct cgp_relu_args {
     const void* xx;      /* [n1][hw] variances at the ReLU input */
     const void* yy;      /* [n2][hw] */
     int64_t nmaps, n1, n2;
-    int32_t hw, same, diag, reserved;
+    int32_t hw, same, diag, flags;   /* flags: CGP_FLAG_* */
 } cgp_relu_args;
 int cgp_relu_f64(const cgp_relu_args* args, void* stream);
 int cgp_relu_f32(const cgp_relu_args* args, void* stream);

@@ -19,8 +19,13 @@ import configs_util
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-RTOL64 = 1e-10
+# float64 kernel entries vs the reference: the op-by-op ReLU ("exact") agrees to 1e-10;
+# the closed-form ReLU (default, "fast") is within 1e-14 of the exact map but the
+# reference's acos(rho) near |rho| = 1 carries ~1e-8 of its own noise (SURVEY.md §4,
+# tests/test_relu_closed_form.py), so entries agree to 1e-8.  North star: 1e-5.
+RTOL64 = {"exact": 1e-10, "fast": 1e-8}
 RTOL32 = 2e-5
+NUMERICS = ["fast", "exact"]
 
 
 def load(name):
@@ -44,7 +49,7 @@ def rel_err(got, ref):
 # Conv2d covariance stencil against the reference's Conv2d.propagate
 # ------------------------------------------------------------------------------------
 def conv_direct(maps, spec, pre=0, post=0, addend=None, pre_var=None, post_var=None,
-                n1=None, n2=None, same=0, diag=0, mpb=0, dtype=torch.float64):
+                n1=None, n2=None, same=0, diag=0, mpb=0, dtype=torch.float64, flags=0):
     g = O.conv_geometry(spec)
     P, H, W = maps.shape
     Ho, Wo = O.conv_out_size(H, g), O.conv_out_size(W, g)
@@ -60,6 +65,7 @@ def conv_direct(maps, spec, pre=0, post=0, addend=None, pre_var=None, post_var=N
     a.weight = float(O.conv_weight(spec, np.float64))
     a.bias = float(spec.get("var_bias", 0.0))
     a.pre, a.post, a.same, a.diag, a.maps_per_block = pre, post, same, diag, mpb
+    a.flags = flags
     keep = []
     if addend is not None:
         t = dev(addend, dtype)
@@ -85,13 +91,15 @@ def par_spec(par):
                 dilation=int(d), var_weight=float(vw), var_bias=float(vb))
 
 
-def test_conv_golden_cases():
+@pytest.mark.parametrize("path", ["fast", "generic"])
+def test_conv_golden_cases(path):
     z = load("conv_ops.npz")
     keys = sorted({k.rsplit("_", 1)[0] for k in z.files})
     worst = 0.0
     for k in keys:
         spec = par_spec(z[k + "_par"])
-        got = conv_direct(z[k + "_in"].astype(np.float64), spec)
+        got = conv_direct(z[k + "_in"].astype(np.float64), spec,
+                          flags=N.CGP_FLAG_GENERIC_CONV if path == "generic" else 0)
         ref = z[k + "_out"]
         assert got.shape == ref.shape, k
         err = rel_err(got, ref)
@@ -101,13 +109,53 @@ def test_conv_golden_cases():
 
 
 @pytest.mark.parametrize("mpb", [1, 3, 7, 0])
-def test_conv_chunking_and_ragged_tail(mpb):
+@pytest.mark.parametrize("flags", [0, 2])
+def test_conv_chunking_and_ragged_tail(mpb, flags):
     rng = np.random.default_rng(mpb)
     maps = rng.random((37, 14, 14))
     spec = dict(kernel_size=3, stride=2, padding="same", dilation=1, var_weight=3.0,
                 var_bias=0.25)
-    got = conv_direct(maps, spec, mpb=mpb)
+    got = conv_direct(maps, spec, mpb=mpb, flags=flags)
     np.testing.assert_allclose(got, O.conv_maps(maps, spec), rtol=1e-14, atol=0)
+
+
+# (n1, n2, side, k, stride, mpb): small n2 (a chunk spans several rows i), chunks whose
+# column range wraps, odd map sizes (4-byte DMA path), stride 2, even kernels
+FUSED_CASES = [(5, 4, 12, 5, 1, 0), (3, 2, 7, 3, 1, 5), (4, 3, 7, 3, 2, 0),
+               (6, 5, 9, 4, 1, 3), (2, 7, 14, 7, 1, 2), (3, 1, 6, 2, 2, 4),
+               (4, 4, 8, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES)
+@pytest.mark.parametrize("flags", [0, 2, 1])
+@pytest.mark.parametrize("diag", [0, 1])
+def test_fused_geometries(case, flags, diag):
+    """every fusion (PRE relu, POST relu, addend) on the fast path (flags 0), the generic
+    path (2) and with the exact ReLU (1), against the oracle"""
+    n1, n2, side, k, st, mpb = case
+    if diag:
+        n2 = n1
+    rng = np.random.default_rng(n1 * 100 + side)
+    X = rng.random((n1, 2, side, side))
+    Y = rng.random((n2, 2, side, side))
+    kp = O.moments(X, Y, False, bool(diag))
+    spec = dict(kernel_size=k, stride=st, padding="same", dilation=1, var_weight=2.0,
+                var_bias=0.5)
+    r1 = O.relu(kp)
+    c = O._conv_kp(r1, spec, "f32")
+    r2 = O.relu(c)
+    addend = rng.random(r2["xy"].shape)
+    ref = r2["xy"] + addend
+    got = conv_direct(kp["xy"], spec, pre=1, post=1, addend=addend,
+                      pre_var=(kp["xx"], kp["yy"]), post_var=(c["xx"], c["yy"]),
+                      n1=n1, n2=n2, diag=diag, mpb=mpb, flags=flags)
+    assert rel_err(got, ref) < 1e-12
+    # no fusion at all, and POST-only
+    got = conv_direct(r1["xy"], spec, n1=n1, n2=n2, diag=diag, mpb=mpb, flags=flags)
+    assert rel_err(got, c["xy"]) < 1e-14
+    got = conv_direct(r1["xy"], spec, post=1, post_var=(c["xx"], c["yy"]), n1=n1, n2=n2,
+                      diag=diag, mpb=mpb, flags=flags)
+    assert rel_err(got, r2["xy"]) < 1e-12
 
 
 def _pair_kp(n1, n2, side, rng, same=False):
@@ -133,7 +181,7 @@ def test_fused_pre_relu_post_relu_add(same):
     got = conv_direct(kp["xy"], spec, pre=1, post=1, addend=addend,
                       pre_var=(kp["xx"], kp["yy"]), post_var=(c["xx"], c["yy"]),
                       n1=n1, n2=n2, same=int(same))
-    assert rel_err(got, ref) < 1e-12
+    assert rel_err(got, ref) < 1e-12       # random data: |rho| well inside (-1, 1)
 
 
 def test_fused_moments():
@@ -163,7 +211,8 @@ def test_fused_moments():
 @pytest.mark.parametrize("dt", ["f64", "f32"])
 @pytest.mark.parametrize("same", [0, 1])
 @pytest.mark.parametrize("diag", [0, 1])
-def test_relu_golden(dt, same, diag):
+@pytest.mark.parametrize("numerics", NUMERICS)
+def test_relu_golden(dt, same, diag, numerics):
     z = load("relu_ops.npz")
     key = f"{dt}_s{same}_d{diag}"
     tdt = torch.float64 if dt == "f64" else torch.float32
@@ -175,6 +224,7 @@ def test_relu_golden(dt, same, diag):
     r = N.ReluArgs()
     r.xy, r.out, r.xx, r.yy = N.ptr(xyd), N.ptr(out), N.ptr(xxd), N.ptr(yyd)
     r.nmaps, r.n1, r.n2, r.hw, r.same, r.diag = xy.shape[0], n1, n2, hw, same, diag
+    r.flags = N.CGP_FLAG_EXACT_RELU if numerics == "exact" else 0
     fn = N.load().cgp_relu_f64 if dt == "f64" else N.load().cgp_relu_f32
     N.check(fn(ctypes.byref(r), stream()), "relu")
     tol = 1e-12 if dt == "f64" else 2e-6
@@ -187,16 +237,23 @@ def test_relu_golden(dt, same, diag):
     np.testing.assert_array_equal(yo.cpu().numpy(), z[key + "_oyy"])
 
 
-def test_relu_known_answers():
+@pytest.mark.parametrize("numerics", NUMERICS)
+def test_relu_known_answers(numerics):
     z = load("relu_ops.npz")
     c, v1, v2 = dev(z["known_c"]), dev(z["known_v1"]), dev(z["known_v2"])
     out = torch.empty_like(c)
     r = N.ReluArgs()
     r.xy, r.out, r.xx, r.yy = N.ptr(c), N.ptr(out), N.ptr(v1), N.ptr(v2)
     r.nmaps, r.n1, r.n2, r.hw, r.same, r.diag = 4, 4, 4, 1, 0, 1
+    r.flags = N.CGP_FLAG_EXACT_RELU if numerics == "exact" else 0
     N.check(N.load().cgp_relu_f64(ctypes.byref(r), stream()), "relu")
     o = out.cpu().numpy()
-    np.testing.assert_allclose(o, z["known_out"], rtol=1e-12, atol=0)
+    # c = +sqrt(v1 v2): the reference is 4e-9 off the exact sqrt(6)/2 (acos near 1)
+    # (rho = -1: the exact value is 0; the reference returns 4.7e-9 there — compare on
+    # the map's natural scale sqrt(v1 v2))
+    scale = np.sqrt(z["known_v1"] * z["known_v2"]) + 1e-300
+    tol = 1e-12 if numerics == "exact" else 1e-8
+    assert (np.abs(o - z["known_out"]) <= tol * np.maximum(scale, np.abs(z["known_out"]))).all()
     assert abs(o[3] - 1.7255613506e-20) / 1.7255613506e-20 < 1e-9   # sqrt(f32 tiny)/2π
 
 
@@ -208,11 +265,13 @@ CFGS = ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp", "mnist_as_tf", 
 
 @pytest.mark.parametrize("cfg", CFGS)
 @pytest.mark.parametrize("dtn", ["f64", "f32"])
-def test_e2e_matches_reference_golden(cfg, dtn):
+@pytest.mark.parametrize("numerics", NUMERICS)
+def test_e2e_matches_reference_golden(cfg, dtn, numerics):
     z = load(f"e2e_{cfg}.npz")
     tdt = torch.float64 if dtn == "f64" else torch.float32
-    model = configs_util.model(cfg).to(DEV, tdt)
-    tol = RTOL64 if dtn == "f64" else RTOL32
+    model = configs_util.model(cfg).to(DEV, tdt).set_exact_relu(numerics == "exact")
+    tol = RTOL64[numerics] if dtn == "f64" else RTOL32
+    worst = 0.0
     prefixes = sorted({k.rsplit("_", 1)[0] for k in z.files if k.endswith("_X")})
     for pre in prefixes:
         X, Z = dev(z[pre + "_X"], tdt), dev(z[pre + "_Z"], tdt)
@@ -226,7 +285,9 @@ def test_e2e_matches_reference_golden(cfg, dtn):
         for name, t in got.items():
             assert t.dtype == tdt and t.device.type == "cuda"
             err = rel_err(t.cpu().numpy(), z[f"{pre}_{dtn}_{name}"])
+            worst = max(worst, err)
             assert err < tol, (cfg, pre, dtn, name, err)
+    print(f"{cfg} {dtn} {numerics}: worst rel err vs reference {worst:.2e}")
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -249,7 +310,7 @@ def test_cpu_inputs_round_trip_to_host():
     X = torch.from_numpy(z["s0_mnist_X"]).double()
     K = m(X)
     assert K.device.type == "cpu"
-    assert rel_err(K.numpy(), z["s0_mnist_f64_Kxx"]) < RTOL64
+    assert rel_err(K.numpy(), z["s0_mnist_f64_Kxx"]) < RTOL64["fast"]
 
 
 def test_mixture_against_oracle():
@@ -281,10 +342,10 @@ def test_edge_shapes_and_zero_images():
         a, b = X[:n1], X[-n2:]
         ref = O.kernel(spec, a, b, False, False)
         got = m(dev(a), dev(b), False, False).cpu().numpy()
-        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-300)
+        np.testing.assert_allclose(got, ref, rtol=RTOL64["fast"], atol=1e-300)
     ref = O.kernel(spec, X)
     got = m(dev(X)).cpu().numpy()
-    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-300)
+    np.testing.assert_allclose(got, ref, rtol=RTOL64["fast"], atol=1e-300)
     # same-tile diagonal override: K[1,1] = xx/2 chain of a zero image is exactly 0;
     # off the diagonal the f32_tiny term keeps zero-variance pairs strictly positive
     assert got[1, 1] == ref[1, 1] == 0.0

@@ -44,6 +44,11 @@ def test_struct_layouts_match():
     assert lib.cgp_abi_version() == N.CGP_ABI_VERSION
 
 
+def test_library_selftest():
+    lib = N.load()
+    assert lib.cgp_selftest() == 0, lib.cgp_last_error()
+
+
 def test_device_count_without_gpu_is_safe():
     assert N.load().cgp_device_count() >= 0
 
