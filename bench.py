@@ -221,6 +221,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_solve:
         labels = torch.randint(0, 10, (n_total,), generator=g)
         Y = cnn_gp.one_hot_pm1(labels, 10).to(dev)
+        # untimed warm-up solve (rocBLAS/rocSOLVER load their kernels on first use)
+        cnn_gp.solve_system(K[:256, :256].clone(), Y[:256], jitter=1e-6)
         Kc = K.clone()
         torch.cuda.synchronize()
         t1 = time.perf_counter()

@@ -4,7 +4,7 @@
 reference's configs (configs/*.py:2-16); ``model(x, x2, same, diag)`` evaluates the
 NNGP kernel with hand-written HIP kernels (libcnngp.so).
 """
-from . import kernels, data, kernel_save_tools, solve
+from . import kernels, data, kernel_save_tools, solve, gram
 from .kernels import *  # noqa: F401,F403
 from .data import *  # noqa: F401,F403
 from .kernel_save_tools import *  # noqa: F401,F403

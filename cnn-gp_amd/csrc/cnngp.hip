@@ -108,6 +108,7 @@ template <> struct K<double> {
     static constexpr double tiny = 1.1754943508222875e-38;   // np.finfo(np.float32).tiny
     static constexpr double xfloor = 1e-300;
 };
+// (fast path) floors keep rsq finite at x = 0; the product is multiplied by x = 0 anyway
 template <> struct K<float> {
     static constexpr float pi = 3.14159265358979f;
     static constexpr float two_pi = 6.28318530717959f;
@@ -132,19 +133,15 @@ __device__ __noinline__ T relu_exact(T c, T v1, T v2) {
     return (s + (K<T>::pi - th) * c) / K<T>::two_pi;        // :152
 }
 
-// rsqrt(t) to full precision: hardware estimate + Newton steps y += y(1 - t y²)/2
-__device__ __forceinline__ double rsqrt_full(double t) {
-    double y = __builtin_amdgcn_rsq(t);
-    double e = __builtin_fma(-t * y, y, 1.0);
-    y = __builtin_fma(0.5 * y, e, y);
-    e = __builtin_fma(-t * y, y, 1.0);
+// rsqrt(t): hardware estimate refined by one Newton step y += y(1 - t y²)/2.  Measured on
+// MI355X (tools/probes/rsq_probe.hip): v_rsq_f64 5.2e-8 -> 4.2e-15 after one step;
+// v_rsq_f32 is 9.4e-8 raw (float rounding level), used as is.
+__device__ __forceinline__ double rsqrt_fast(double t) {
+    const double y = __builtin_amdgcn_rsq(t);
+    const double e = __builtin_fma(-t * y, y, 1.0);
     return __builtin_fma(0.5 * y, e, y);
 }
-__device__ __forceinline__ float rsqrt_full(float t) {
-    float y = __builtin_amdgcn_rsqf(t);
-    const float e = __builtin_fmaf(-t * y, y, 1.0f);
-    return __builtin_fmaf(0.5f * y, e, y);
-}
+__device__ __forceinline__ float rsqrt_fast(float t) { return __builtin_amdgcn_rsqf(t); }
 __device__ __forceinline__ double relu_poly(double u) {
     double r = kReluPolyD[kReluPolyDegD];
 #pragma unroll
@@ -157,21 +154,32 @@ __device__ __forceinline__ float relu_poly(float u) {
     for (int k = kReluPolyDegF - 1; k >= 0; --k) r = __builtin_fmaf(r, u, kReluPolyF[k]);
     return r;
 }
+__device__ __forceinline__ double fmin_t(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ float fmin_t(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double fmax_t(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float fmax_t(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ double fabs_t(double a) { return __builtin_fabs(a); }
+__device__ __forceinline__ float fabs_t(float a) { return __builtin_fabsf(a); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) {
+    return __builtin_fma(a, b, c);
+}
+__device__ __forceinline__ float fma_t(float a, float b, float c) {
+    return __builtin_fmaf(a, b, c);
+}
 
 template <typename T>
 __device__ __forceinline__ T relu_fast(T c, T v1, T v2) {
     const T t = v1 * v2 + K<T>::tiny;
-    const T y = rsqrt_full(t);
+    const T y = rsqrt_fast(t);
     const T st = t * y;                                     // sqrt(t)
-    T a = c * y;
-    a = a < T(0) ? -a : a;
-    a = a > T(1) ? T(1) : a;                                // |rho| clamped, NaN kept
-    const T x = T(0.5) - T(0.5) * a;                        // (1 - a)/2
-    const T xs = x > K<T>::xfloor ? x : K<T>::xfloor;
-    const T sx = xs * rsqrt_full(xs);                       // sqrt(x)
-    const T p = relu_poly(T(4) * x - T(1));
-    const T pos = c > T(0) ? c : T(0);
-    return (st * x) * sx * p + T(0.5) * pos;
+    const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
+    const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
+    const T xs = fmax_t(x, K<T>::xfloor);
+    const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
+    const T p = relu_poly(fma_t(T(4), x, T(-1)));
+    const T pos = fmax_t(c, T(0));
+    // (c - c): 0 for finite c, NaN for NaN c — keeps the reference's NaN propagation
+    return fma_t((st * x) * sx, p, T(0.5) * pos) + (c - c);
 }
 
 // ReLU of pair map m at pixel px with the same/diag overrides of kernels.py:155-162.
@@ -404,6 +412,7 @@ struct Geo {
     static constexpr int HW = H * W, HOWO = HO * WO;
     static constexpr int PLO = OFF < 0 ? -OFF : 0;
     static constexpr int R3 = HO >= 8 ? 4 : (HO >= 2 ? 2 : 1);   // rows per stage-3 item
+    static constexpr int R2 = WO % 4 == 0 ? 4 : (WO % 2 == 0 ? 2 : 1);   // cols per stage-2 item
     static constexpr int HOS = (HO + R3 - 1) / R3 * R3;
     static constexpr int LASTC = (WO - 1) * S + OFF + TAPS - 1;
     static constexpr int LASTR = (HOS - 1) * S + OFF + TAPS - 1;
@@ -412,7 +421,43 @@ struct Geo {
     static constexpr int C0 = OFF + PLO, R0 = OFF + PLO;
     static constexpr int PL = HP * WP;
     static constexpr int WIN = (R3 - 1) * S + TAPS;               // stage-3 register window
+    static constexpr int WIN2 = (R2 - 1) * S + TAPS;              // stage-2 register window
 };
+
+// out[o] = sum_{t<TAPS} w[o*S + t] for o < R, sharing partial sums between the R
+// overlapping windows (stride 1): the core w[R-1 .. TAPS-1] is common to every output,
+// so R outputs cost (TAPS - R) + R(R - 1) adds instead of R(TAPS - 1).
+template <typename T, int TAPS, int S, int R>
+__device__ __forceinline__ void window_sums(const T (&w)[(R - 1) * S + TAPS], T (&out)[R]) {
+    if constexpr (S == 1 && TAPS > R && R > 1) {
+        T core = w[R - 1];
+#pragma unroll
+        for (int t = R; t < TAPS; ++t) core += w[t];
+#pragma unroll
+        for (int o = 0; o < R; ++o) {
+            T acc;
+            if (o < R - 1) {
+                acc = w[o];
+#pragma unroll
+                for (int t = o + 1; t < R - 1; ++t) acc += w[t];
+                acc += core;
+            } else {
+                acc = core;
+            }
+#pragma unroll
+            for (int t = TAPS; t < TAPS + o; ++t) acc += w[t];
+            out[o] = acc;
+        }
+    } else {
+#pragma unroll
+        for (int o = 0; o < R; ++o) {
+            T acc = w[o * S];
+#pragma unroll
+            for (int t = 1; t < TAPS; ++t) acc += w[o * S + t];
+            out[o] = acc;
+        }
+    }
+}
 
 constexpr int cround(int n, int a) { return (n + a - 1) / a * a; }
 
@@ -525,8 +570,9 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::PW) : "memory");
         lds_barrier();
 
+        const T* addend_c = ADD ? p.addend + m0 * G::HOWO : nullptr;
         // variance / addend values this thread's stage-3 outputs need (loaded now, used
-        // after stage 2; the compiler counts the DMA issued in between)
+        // after stage 2)
         T vx[L::I3][G::R3], vy[L::I3][G::R3], ad[L::I3][G::R3];
         unsigned pi[L::I3], pj[L::I3];
 #pragma unroll
@@ -541,15 +587,18 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
             pair_of((unsigned)(m0 + ml), p.n2, p.diag, i, j);
             pi[k] = i;
             pj[k] = j;
+            // 32-bit element offsets from scalar bases (saddr + voffset addressing)
+            const unsigned xo = i * (unsigned)G::HOWO, yo = j * (unsigned)G::HOWO;
+            const unsigned ao = (unsigned)(ml * G::HOWO);
 #pragma unroll
             for (int o = 0; o < G::R3; ++o) {
                 const int oh = oh0 + o < G::HO ? oh0 + o : G::HO - 1;
-                const int q = oh * G::WO + ow;
+                const unsigned q = (unsigned)(oh * G::WO + ow);
                 if constexpr (POST) {
-                    vx[k][o] = p.post_xx[(size_t)i * G::HOWO + q];
-                    vy[k][o] = p.post_yy[(size_t)j * G::HOWO + q];
+                    vx[k][o] = p.post_xx[xo + q];
+                    vy[k][o] = p.post_yy[yo + q];
                 }
-                if constexpr (ADD) ad[k][o] = p.addend[(m0 + ml) * G::HOWO + q];
+                if constexpr (ADD) ad[k][o] = addend_c[ao + q];
             }
         }
 
@@ -581,15 +630,19 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
         }
         lds_barrier();
 
-        // ---- stage 2: row sums (every padded row), one output per item ----
-        for (int e = tid; e < mb * G::HP * G::WO; e += kBlock) {
-            const int rowi = e / G::WO;                           // ml * HP + rp
-            const int ow = e - rowi * G::WO;
-            const T* src = plane + rowi * G::WP + ow * G::S + G::C0;
-            T acc = src[0];
+        // ---- stage 2: row sums (every padded row), R2 outputs per item ----
+        constexpr int NSEG2 = G::WO / G::R2;
+        for (int e = tid; e < mb * G::HP * NSEG2; e += kBlock) {
+            const int rowi = e / NSEG2;                           // ml * HP + rp
+            const int seg = e - rowi * NSEG2;
+            const T* src = plane + rowi * G::WP + seg * (G::R2 * G::S) + G::C0;
+            T win[G::WIN2];
 #pragma unroll
-            for (int t = 1; t < G::TAPS; ++t) acc += src[t];
-            hs[e] = acc;
+            for (int t = 0; t < G::WIN2; ++t) win[t] = src[t];
+            T res[G::R2];
+            window_sums<T, G::TAPS, G::S, G::R2>(win, res);
+#pragma unroll
+            for (int o = 0; o < G::R2; ++o) hs[rowi * G::WO + seg * G::R2 + o] = res[o];
         }
         lds_barrier();
 
@@ -608,13 +661,9 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
 #pragma unroll
                 for (int t = 0; t < G::WIN; ++t) win[t] = src[t * G::WO];
                 T res[G::R3];
+                window_sums<T, G::TAPS, G::S, G::R3>(win, res);
 #pragma unroll
-                for (int o = 0; o < G::R3; ++o) {
-                    T acc = win[o * G::S];
-#pragma unroll
-                    for (int t = 1; t < G::TAPS; ++t) acc += win[o * G::S + t];
-                    res[o] = p.weight * acc + p.bias;
-                }
+                for (int o = 0; o < G::R3; ++o) res[o] = p.weight * res[o] + p.bias;
                 if constexpr (POST) {
                     const bool ovr = p.same && (p.diag || pi[k] == pj[k]);
 #pragma unroll
@@ -633,7 +682,8 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
                 }
 #pragma unroll
                 for (int o = 0; o < G::R3; ++o) {
-                    if (oh0 + o < G::HO) out[ml * G::HOWO + (oh0 + o) * G::WO + ow] = res[o];
+                    if (oh0 + o < G::HO)
+                        out[(unsigned)(ml * G::HOWO + (oh0 + o) * G::WO + ow)] = res[o];
                 }
             }
         }
