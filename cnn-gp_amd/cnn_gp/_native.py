@@ -14,11 +14,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 2
+CGP_ABI_VERSION = 3
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
+CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -49,6 +50,36 @@ class ReluArgs(ctypes.Structure):
     ]
 
 
+class NetOp(ctypes.Structure):
+    """Mirror of cgp_net_op (include/cnngp.h)."""
+    _fields_ = [
+        ("kind", _i32), ("code", _i32), ("src", _i32), ("dst", _i32), ("add", _i32),
+        ("ws_in", _i32), ("ws_out", _i32), ("relu", _i32), ("h", _i32), ("w", _i32),
+        ("div_m", ctypes.c_uint32), ("div_s", ctypes.c_uint32),
+        ("weight", _f64), ("bias", _f64), ("var_x", _vp), ("var_y", _vp),
+    ]
+
+
+class NetArgs(ctypes.Structure):
+    """Mirror of cgp_net_args (include/cnngp.h)."""
+    _fields_ = [
+        ("x", _vp), ("y", _vp), ("out", _vp), ("kdiag", _vp), ("ops", _vp),
+        ("n1", _i64), ("n2", _i64), ("ldo", _i64),
+        ("nops", _i32), ("channels", _i32), ("h", _i32), ("w", _i32),
+        ("same", _i32), ("final_slot", _i32), ("hs", _i32), ("lds_elems", _i32),
+        ("flags", _i32), ("reserved", _i32),
+    ]
+
+
+def make_fastdiv(d: int):
+    """(m, s) of the multiply-high divisor the kernels use (cgp_common.h FastDiv)."""
+    s = 0
+    while (1 << s) < d:
+        s += 1
+    m = (((1 << 32) * ((1 << s) - d)) // d + 1) & 0xFFFFFFFF
+    return m, s
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "cgp_abi_version": (_i32, []),
@@ -75,6 +106,13 @@ SIGNATURES = {
                                   ctypes.POINTER(_i64), _vp]),
     "cgp_gemm_f64": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "cgp_net_geometry": (_i32, [_i32] * 7),
+    "cgp_net_hs_elems": (_i32, [_i32]),
+    "cgp_net_op_size": (ctypes.c_size_t, []),
+    "cgp_net_args_size": (ctypes.c_size_t, []),
+    "cgp_net_occupancy": (_i32, [_i32, _i32]),
+    "cgp_net_f64": (_i32, [ctypes.POINTER(NetArgs), _vp]),
+    "cgp_net_f32": (_i32, [ctypes.POINTER(NetArgs), _vp]),
 }
 
 _lib = None
@@ -108,7 +146,9 @@ def load():
             _lib_err = "libcnngp.so ABI version mismatch (rebuild it)"
             raise RuntimeError(_lib_err)
         if lib.cgp_conv_args_size() != ctypes.sizeof(ConvArgs) or \
-                lib.cgp_relu_args_size() != ctypes.sizeof(ReluArgs):
+                lib.cgp_relu_args_size() != ctypes.sizeof(ReluArgs) or \
+                lib.cgp_net_op_size() != ctypes.sizeof(NetOp) or \
+                lib.cgp_net_args_size() != ctypes.sizeof(NetArgs):
             _lib_err = "libcnngp.so argument struct layout differs from _native.py"
             raise RuntimeError(_lib_err)
         _lib = lib

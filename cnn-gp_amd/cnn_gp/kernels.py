@@ -61,6 +61,28 @@ class NNGPKernel(nn.Module):
             m.__dict__["_cgp_fusion"] = bool(enabled)
         return self
 
+    def set_fused_network(self, enabled: bool):
+        """Run off-diagonal forwards on the whole-network kernel (csrc/netfuse.hip: one
+        workgroup carries a pair's map through every layer in LDS; default) or on the
+        layer-by-layer pipeline (one HBM pass per fused op).  Models the fused kernel
+        has no instantiation for use the layer path either way."""
+        for m in self.modules():
+            m.__dict__["_cgp_netfuse"] = bool(enabled)
+        return self
+
+    def _net_plan(self, plan, itemsize):
+        """The NetPlan of ``plan`` or None (unsupported program / disabled)."""
+        if not getattr(self, "_cgp_netfuse", True):
+            return None
+        key = ("_net", itemsize)
+        if key not in plan.__dict__:
+            from .netplan import NetPlan, Unsupported
+            try:
+                plan.__dict__[key] = NetPlan(plan, itemsize)
+            except Unsupported:
+                plan.__dict__[key] = None
+        return plan.__dict__[key]
+
     def set_exact_relu(self, enabled: bool):
         """Evaluate the ReLU map op by op exactly like the reference (correctly rounded
         1/sqrt, sqrt, acos, division) instead of the closed form (default; within 1e-14 of
@@ -111,6 +133,11 @@ class NNGPKernel(nn.Module):
         N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, c, h * w,
                                                         N.ptr(var0[:n1]), N.ptr(var0[n1:]),
                                                         stream), "cgp_moments_var")
+        net = None if diag else self._net_plan(plan, x.element_size())
+        if net is not None:                                      # whole-network kernel
+            var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, stream,
+                                     need=net.need_var)
+            return net.run(x, y, var, n1, n2, same, stream, plan.flags)
         var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, stream)
         xy0 = None
         if not plan.moments_fused:

@@ -1,0 +1,250 @@
+"""Lowering of a compiled program to the whole-network pair kernel (cgp_net_*).
+
+The layer-by-layer pair pipeline (program.Plan.run_pairs) writes every intermediate
+[N1·N2, H, W] map to HBM.  ``NetPlan`` instead lowers the SAME SSA program
+(program.compile_program) to a list of ``cgp_net_op`` over LDS slots, executed per pair
+by one workgroup (csrc/netfuse.hip).  Semantics per op, with the reference lines:
+
+    MOMENTS  v0 = mean_c x_i·y_j                              kernels.py:44-47
+    CONV     w·Σ_window + b [→ ReLU] [+ addend]               kernels.py:92-98, 134-165
+    RELU     relu(src) [+ addend]                             kernels.py:134-165
+    LINEAR   a·src + b·add   (Sum / Mixture terms)           kernels.py:220-254
+
+Fusion uses rules 1-2 of program.fuse (conv→ReLU epilogue, 2-term Sum folded into its
+producer); both are exact (IEEE addition commutes).  A ReLU feeding two consumers and the
+input moments stay standalone ops: in LDS they cost no extra memory pass.
+
+Slots.  Every value lives in a slot of its spatial class (H, W): a row-major plane with
+HL zero columns left and HR right of each row (the widest halo any conv reading that
+class needs), row stride ws = HL + W + HR.  Halos are zeroed once per workgroup and never
+written, so convs read padding as zeros.  Rows need no halo: the conv's row-sum scratch
+carries zero rows instead.  Slots are reused as soon as their value is dead, including
+in place (dst == src) — safe because every op reads a pixel before the same thread
+writes it, and convs consume their whole input into the scratch before writing.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional
+
+import torch
+
+from . import _native as N
+from .program import fuse
+
+ALIGN = 2                      # slot bases on 16-byte boundaries (fp64 elements)
+MAX_LDS_BYTES = 160 * 1024
+
+
+class Unsupported(Exception):
+    """The program cannot run on the whole-network kernel (layer path instead)."""
+
+
+@dataclasses.dataclass
+class _Slot:
+    base: int                  # element offset of the slot
+    origin: int                # element offset of pixel (0, 0)
+    cls: tuple                 # (H, W)
+
+
+def _conv_halo(op):
+    """(left, right) zero columns the conv reads beyond its input row."""
+    g = op.geom
+    w = op.shape_in[1]
+    wo = op.shape_out[1]
+    left = max(0, -g.offset)
+    right = max(0, (wo - 1) * g.stride + g.offset + (g.taps - 1) * g.dilation - (w - 1))
+    return left, right
+
+
+class NetPlan:
+    """The whole-network kernel program for one Plan (one model at one input size)."""
+
+    def __init__(self, plan, itemsize: int = 8):
+        self.plan = plan
+        prog, v0, vf = plan.prog, plan.v0, plan.vf
+        if plan.final_hw != (1, 1):
+            raise Unsupported(f"final map is {plan.final_hw}, not 1x1")
+        ops = fuse(prog, v0, vf, True, pre_relu=False, fold_moments=False)
+        lib = N.load()
+        # 1. per-op checks + geometry codes
+        hs_need = 2
+        codes = {}
+        for k, op in enumerate(ops):
+            if op.kind == "conv":
+                g = op.geom
+                if g.dilation != 1:
+                    raise Unsupported("dilated conv")
+                (h, w), (ho, wo) = op.shape_in, op.shape_out
+                code = lib.cgp_net_geometry(h, w, ho, wo, g.taps, g.stride, g.offset)
+                if code < 0:
+                    raise Unsupported(f"conv geometry {(h, w, ho, wo, g.taps, g.stride, g.offset)}"
+                                      " has no fused instantiation")
+                codes[k] = code
+                hs_need = max(hs_need, lib.cgp_net_hs_elems(code))
+            elif op.kind in ("relu", "add"):
+                pass
+            else:
+                raise Unsupported(f"op {op.kind}")
+        # 2. slot classes and their halos
+        shapes = prog.shapes
+        halo = {}
+        for v, shp in shapes.items():
+            halo.setdefault(tuple(shp), [0, 0])
+        for op in ops:
+            if op.kind == "conv":
+                lft, rgt = _conv_halo(op)
+                hl = halo[tuple(op.shape_in)]
+                hl[0] = max(hl[0], lft)
+                hl[1] = max(hl[1], rgt)
+        self.ws = {c: hl[0] + c[1] + hl[1] for c, hl in halo.items()}
+
+        def slot_elems(c):
+            n = c[0] * self.ws[c]
+            return (n + ALIGN - 1) // ALIGN * ALIGN
+
+        # 3. lower to a linear op list with explicit LINEAR chains
+        lowered = [("moments", v0, None)]
+        for k, op in enumerate(ops):
+            lowered.append(("op", k, op))
+        last = {}
+        for idx, (kind, a, op) in enumerate(lowered):
+            if kind == "op":
+                srcs = ([op.src] if op.src is not None else []) + [t for _, t in op.terms]
+                if op.addend is not None:
+                    srcs.append(op.addend)
+                for s in srcs:
+                    last[s] = idx
+        last[vf] = len(lowered)
+        # 4. slot allocation (linear scan, per class free lists, in-place allowed)
+        free: dict = {}
+        slots: dict = {}
+        top = 0
+        self.hs = 0
+        top = (hs_need + ALIGN - 1) // ALIGN * ALIGN
+
+        def alloc(v):
+            nonlocal top
+            c = tuple(shapes[v])
+            lst = free.get(c)
+            if lst:
+                sl = lst.pop()
+            else:
+                hl = halo[c][0]
+                sl = _Slot(top, top + hl, c)
+                top += slot_elems(c)
+            slots[v] = sl
+            return sl
+
+        def release_dead(idx):
+            for v in [v for v, sl in slots.items() if last.get(v, -1) == idx and v != vf]:
+                free.setdefault(slots[v].cls, []).append(slots.pop(v))
+
+        recs = []           # (NetOp fields dict, var value or None)
+        for idx, (kind, a, op) in enumerate(lowered):
+            if kind == "moments":
+                h, w = shapes[v0]
+                release_dead(idx)
+                d = alloc(v0)
+                recs.append((dict(kind=N.CGP_NET_MOMENTS, src=0, dst=d.origin, add=-1,
+                                  ws_in=self.ws[(h, w)], ws_out=self.ws[(h, w)], h=h, w=w),
+                             None))
+                continue
+            k = a
+            if op.kind == "conv":
+                s = slots[op.src]
+                ad = slots[op.addend].origin if op.addend is not None else -1
+                release_dead(idx)
+                d = alloc(op.dst)
+                ho, wo = op.shape_out
+                relu = op.post == N.CGP_POST_RELU
+                recs.append((dict(kind=N.CGP_NET_CONV, code=codes[k], src=s.origin,
+                                  dst=d.origin, add=ad, ws_in=self.ws[tuple(op.shape_in)],
+                                  ws_out=self.ws[(ho, wo)], relu=int(relu), h=ho, w=wo,
+                                  weight=op.geom.weight, bias=op.geom.bias,
+                                  geom=(*op.shape_in, ho, wo, op.geom.taps, op.geom.stride,
+                                        op.geom.offset)),
+                             op.post_var if relu else None))
+            elif op.kind == "relu":
+                s = slots[op.src]
+                ad = slots[op.addend].origin if op.addend is not None else -1
+                release_dead(idx)
+                d = alloc(op.dst)
+                h, w = op.shape_out
+                recs.append((dict(kind=N.CGP_NET_RELU, src=s.origin, dst=d.origin, add=ad,
+                                  ws_in=self.ws[(h, w)], ws_out=self.ws[(h, w)], relu=1,
+                                  h=h, w=w), op.src))
+            else:   # add: dst = c0·t0 + c1·t1, then dst = dst + c_k·t_k
+                terms = [(1.0 if c is None else float(c), t) for c, t in op.terms]
+                h, w = op.shape_out
+                srcs = [slots[t].origin for _, t in terms]
+                if len(terms) > 2:          # chained: dst must not alias a later term
+                    d = alloc(op.dst)
+                    release_dead(idx)
+                else:
+                    release_dead(idx)
+                    d = alloc(op.dst)
+                base = dict(kind=N.CGP_NET_LINEAR, dst=d.origin, ws_in=self.ws[(h, w)],
+                            ws_out=self.ws[(h, w)], h=h, w=w)
+                if len(terms) == 1:
+                    recs.append((dict(base, src=srcs[0], add=srcs[0], weight=terms[0][0],
+                                      bias=0.0), None))
+                else:
+                    recs.append((dict(base, src=srcs[0], add=srcs[1], weight=terms[0][0],
+                                      bias=terms[1][0]), None))
+                    for (c, _), so in zip(terms[2:], srcs[2:]):
+                        recs.append((dict(base, src=d.origin, add=so, weight=1.0, bias=c),
+                                     None))
+        self.final_slot = slots[vf].origin
+        self.hs = 0
+        self.lds_elems = top
+        self.records = recs
+        self.need_var = {v for _, v in recs if v is not None} | {vf}
+        self.n_ops = len(recs)
+        if self.lds_elems * itemsize > MAX_LDS_BYTES:
+            raise Unsupported(f"LDS footprint {self.lds_elems * itemsize} B")
+
+    def lds_bytes(self, itemsize: int) -> int:
+        return self.lds_elems * itemsize
+
+    def _ops_array(self, var):
+        arr = (N.NetOp * self.n_ops)()
+        for k, (f, v) in enumerate(self.records):
+            o = arr[k]
+            o.kind = f["kind"]
+            o.code = f.get("code", 0)
+            o.src, o.dst, o.add = f["src"], f["dst"], f["add"]
+            o.ws_in, o.ws_out = f["ws_in"], f["ws_out"]
+            o.relu = f.get("relu", 0)
+            o.h, o.w = f["h"], f["w"]
+            o.div_m, o.div_s = N.make_fastdiv(f["w"])
+            o.weight, o.bias = f.get("weight", 0.0), f.get("bias", 0.0)
+            if v is not None:
+                vx, vy = var[v]
+                o.var_x, o.var_y = vx.data_ptr(), vy.data_ptr()
+        return arr
+
+    def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
+            out: Optional[torch.Tensor] = None):
+        """K tile [n1, n2] of the pairs (x_i, y_j).  var: value -> (xx [n1,..], yy [n2,..])
+        for every value in ``need_var``."""
+        sfx = "f64" if x.dtype == torch.float64 else "f32"
+        arr = self._ops_array(var)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        ops_dev = host.to(x.device)                 # stream-ordered, freed stream-ordered
+        if out is None:
+            out = torch.empty((n1, n2), dtype=x.dtype, device=x.device)
+        a = N.NetArgs()
+        a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
+        if same:
+            kd = var[self.plan.vf][0]
+            a.kdiag = kd.data_ptr()
+        a.ops = ops_dev.data_ptr()
+        a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
+        a.nops, a.channels, a.h, a.w = self.n_ops, x.shape[1], x.shape[2], x.shape[3]
+        a.same, a.final_slot, a.hs, a.lds_elems = int(same), self.final_slot, self.hs, \
+            self.lds_elems
+        a.flags = flags
+        N.check(getattr(N.load(), f"cgp_net_{sfx}")(ctypes.byref(a), stream), "cgp_net")
+        return out

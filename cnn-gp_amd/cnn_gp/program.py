@@ -163,8 +163,11 @@ def _uses(ops, final):
     return u
 
 
-def fuse(prog: Program, v0: int, vf: int, enable: bool = True) -> list:
-    """Return the fused op list for the pair pipeline (prog.ops is left untouched)."""
+def fuse(prog: Program, v0: int, vf: int, enable: bool = True, pre_relu: bool = True,
+         fold_moments: bool = True) -> list:
+    """Return the fused op list for the pair pipeline (prog.ops is left untouched).
+    ``pre_relu`` / ``fold_moments`` enable rules 3 / 4 (the whole-network kernel keeps
+    standalone ReLU and moments ops: in LDS they cost no extra memory pass)."""
     ops = [dataclasses.replace(o, terms=list(o.terms)) for o in prog.ops]
     if not enable:
         return ops
@@ -216,7 +219,7 @@ def fuse(prog: Program, v0: int, vf: int, enable: bool = True) -> list:
                 break
 
     # 3. relu -> conv  ==> conv(pre=RELU) when the relu output has no other consumer
-    changed = True
+    changed = pre_relu
     while changed:
         changed = False
         uses = _uses(ops, vf)
@@ -236,7 +239,7 @@ def fuse(prog: Program, v0: int, vf: int, enable: bool = True) -> list:
 
     # 4. the input moments folded into a single consuming conv
     uses = _uses(ops, vf)
-    if uses.get(v0, 0) == 1 and vf != v0:
+    if fold_moments and uses.get(v0, 0) == 1 and vf != v0:
         for c in ops:
             if c.kind == "conv" and c.src == v0 and c.pre == N.CGP_PRE_NONE:
                 c.pre = N.CGP_PRE_MOMENTS
@@ -294,12 +297,13 @@ class Plan:
         return last
 
     # -- variance pipeline --------------------------------------------------------------
-    def run_variances(self, xx0, yy0, n1, n2, same, stream):
-        """Per-image variance maps of every value a ReLU reads.  xx0/yy0: [n, H, W]."""
+    def run_variances(self, xx0, yy0, n1, n2, same, stream, need=None):
+        """Per-image variance maps of every value a ReLU reads (or of ``need``).
+        xx0/yy0: [n, H, W]."""
         sfx = self._sfx(xx0.dtype)
         dev = xx0.device
         vals = {self.v0: (xx0, yy0)}
-        need = self.need_var
+        need = self.need_var if need is None else need
         ops = self.prog.ops
         last = self._last_use(ops, self.vf)
         keep = {}

@@ -1,0 +1,187 @@
+// cgp_common.h — device math and host plumbing shared by the libcnngp translation
+// units (cnngp.hip: layer-by-layer kernels + C ABI; netfuse.hip: whole-network kernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "cnngp.h"
+#include "relu_poly.h"
+
+namespace cgp {
+
+// error plumbing (no exceptions cross the ABI); defined in cnngp.hip
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+// compute units of the current device (cached; launch geometry of persistent kernels)
+int device_cus();
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define CGP_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(CGP_EHIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_),      \
+                        __FILE__, __LINE__);                                           \
+    } while (0)
+
+
+// ----------------------------------------------------------------------------------
+// n / d for 0 <= n < 2^31 by multiply-high ("division by invariant integers"):
+// q = (umulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1.
+// ----------------------------------------------------------------------------------
+struct FastDiv {
+    unsigned m, s, d;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+    FastDiv f;
+    f.d = d;
+    f.s = 0;
+    while ((1ull << f.s) < d) ++f.s;
+    f.m = (unsigned)(((1ull << 32) * ((1ull << f.s) - d)) / d + 1);
+    return f;
+}
+__host__ __device__ __forceinline__ unsigned umulhi32(unsigned a, unsigned b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umulhi(a, b);
+#else
+    return (unsigned)(((unsigned long long)a * b) >> 32);
+#endif
+}
+__host__ __device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+    return (umulhi32(n, f.m) + n) >> f.s;
+}
+
+// ----------------------------------------------------------------------------------
+// The ReLU covariance map (kernels.py:133-152).
+//
+// relu_exact mirrors the reference op by op: separate roundings (this file is compiled
+// with -ffp-contract=off), torch's clamp NaN propagation, rsqrt as 1/sqrt (ATen's CPU
+// rsqrt), acos, and float constants rounded to T like torch's wrapped Python scalars.
+//
+// relu_fast is the same map in closed form.  With a = |rho| = |c|/sqrt(t) (clamped) and
+// x = (1 - a)/2, acos a = 2 asin sqrt(x) turns (sqrt(t - c²) + (π - acos rho)·c)/2π into
+//     max(c, 0)/2 + sqrt(t) · x · sqrt(x) · P(4x - 1)
+// with P analytic on [0, 1/2] (tools/fit_relu_poly.py; relu_poly.h: degree 15, 3e-15).
+// One branch-free polynomial, two hardware rsq's refined by Newton steps, no division:
+// ~35 double ops instead of ~190 slots for correctly rounded div/sqrt/acos.  Near
+// |rho| = 1 the reference's own acos(rho) is ill-conditioned (~1e-8 relative noise from
+// the last bit of rho); relu_fast evaluates the smooth map there.
+// ----------------------------------------------------------------------------------
+template <typename T> struct K;
+template <> struct K<double> {
+    static constexpr double pi = 3.141592653589793;
+    static constexpr double two_pi = 6.283185307179586;
+    static constexpr double tiny = 1.1754943508222875e-38;   // np.finfo(np.float32).tiny
+    static constexpr double xfloor = 1e-300;
+};
+// (fast path) floors keep rsq finite at x = 0; the product is multiplied by x = 0 anyway
+template <> struct K<float> {
+    static constexpr float pi = 3.14159265358979f;
+    static constexpr float two_pi = 6.28318530717959f;
+    static constexpr float tiny = 1.17549435e-38f;
+    static constexpr float xfloor = 1e-30f;
+};
+
+__device__ __forceinline__ double sqrt_t(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float sqrt_t(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double acos_t(double x) { return acos(x); }
+__device__ __forceinline__ float acos_t(float x) { return acosf(x); }
+
+template <typename T>
+__device__ __forceinline__ T relu_exact_inl(T c, T v1, T v2) {
+    const T t = v1 * v2 + K<T>::tiny;                       // :146
+    T cs = c * (T(1) / sqrt_t(t));                          // :149
+    cs = cs < T(-1) ? T(-1) : (cs > T(1) ? T(1) : cs);      // clamp(-1, 1), NaN kept
+    T d = t - c * c;                                        // :150
+    d = d < T(0) ? T(0) : d;                                // clamp(min=0)
+    const T s = sqrt_t(d);
+    const T th = acos_t(cs);                                // :151
+    return (s + (K<T>::pi - th) * c) / K<T>::two_pi;        // :152
+}
+template <typename T>
+__device__ __noinline__ T relu_exact(T c, T v1, T v2) {
+    return relu_exact_inl(c, v1, v2);
+}
+
+// rsqrt(t): hardware estimate refined by one Newton step y += y(1 - t y²)/2.  Measured on
+// MI355X (tools/probes/rsq_probe.hip): v_rsq_f64 5.2e-8 -> 4.2e-15 after one step;
+// v_rsq_f32 is 9.4e-8 raw (float rounding level), used as is.
+__device__ __forceinline__ double rsqrt_fast(double t) {
+    const double y = __builtin_amdgcn_rsq(t);
+    const double e = __builtin_fma(-t * y, y, 1.0);
+    return __builtin_fma(0.5 * y, e, y);
+}
+__device__ __forceinline__ float rsqrt_fast(float t) { return __builtin_amdgcn_rsqf(t); }
+__device__ __forceinline__ double relu_poly(double u) {
+    double r = kReluPolyD[kReluPolyDegD];
+#pragma unroll
+    for (int k = kReluPolyDegD - 1; k >= 0; --k) r = __builtin_fma(r, u, kReluPolyD[k]);
+    return r;
+}
+__device__ __forceinline__ float relu_poly(float u) {
+    float r = kReluPolyF[kReluPolyDegF];
+#pragma unroll
+    for (int k = kReluPolyDegF - 1; k >= 0; --k) r = __builtin_fmaf(r, u, kReluPolyF[k]);
+    return r;
+}
+__device__ __forceinline__ double fmin_t(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ float fmin_t(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double fmax_t(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float fmax_t(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ double fabs_t(double a) { return __builtin_fabs(a); }
+__device__ __forceinline__ float fabs_t(float a) { return __builtin_fabsf(a); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) {
+    return __builtin_fma(a, b, c);
+}
+__device__ __forceinline__ float fma_t(float a, float b, float c) {
+    return __builtin_fmaf(a, b, c);
+}
+
+template <typename T>
+__device__ __forceinline__ T relu_fast(T c, T v1, T v2) {
+    const T t = v1 * v2 + K<T>::tiny;
+    const T y = rsqrt_fast(t);
+    const T st = t * y;                                     // sqrt(t)
+    const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
+    const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
+    const T xs = fmax_t(x, K<T>::xfloor);
+    const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
+    const T p = relu_poly(fma_t(T(4), x, T(-1)));
+    const T pos = fmax_t(c, T(0));
+    // (c - c): 0 for finite c, NaN for NaN c — keeps the reference's NaN propagation
+    return fma_t((st * x) * sx, p, T(0.5) * pos) + (c - c);
+}
+
+// ReLU of pair map m at pixel px with the same/diag overrides of kernels.py:155-162.
+template <typename T>
+__device__ __forceinline__ T relu_pair(T c, const T* __restrict__ xx, const T* __restrict__ yy,
+                                       unsigned i, unsigned j, int hw, int px, int same,
+                                       int diag, int exact) {
+    const T v1 = xx[(size_t)i * hw + px];
+    if (same && (diag || i == j)) return v1 / T(2);          // xy' = xx' = xx/2
+    const T v2 = yy[(size_t)j * hw + px];
+    return exact ? relu_exact(c, v1, v2) : relu_fast(c, v1, v2);
+}
+
+// pair index -> (i, j)
+__device__ __forceinline__ void pair_of(unsigned m, const FastDiv& n2, int diag, unsigned& i,
+                                        unsigned& j) {
+    if (diag) {
+        i = j = m;
+    } else {
+        i = fdiv(m, n2);
+        j = m - i * n2.d;
+    }
+}
+
+// LDS-only barrier: waits for this wave's LDS traffic, not for its global loads, so the
+// next chunk's prefetch stays in flight across it (cdna_hip_programming.md §5).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+}  // namespace cgp

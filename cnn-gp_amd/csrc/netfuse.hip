@@ -1,0 +1,575 @@
+// netfuse.hip — the whole pair program of a network in ONE kernel (cgp_net_*).
+//
+// The layer-by-layer path (cnngp.hip) streams every pair map through HBM once per fused
+// op: ~100-500 KB of traffic per pair, so it is HBM-bound.  Here one workgroup (two
+// waves) owns one (i, j) pair at a time and runs every op of the network on LDS-resident
+// planes; the only global traffic per pair is the two input images and the per-image
+// variance maps the ReLUs read (both shared by many pairs, so L2/MALL-resident) plus
+// the one K[i, j] it writes.  The kernel is fp64-VALU bound.
+//
+// Reference semantics: moments kernels.py:44-47, Conv2d.propagate kernels.py:92-98,
+// ReLU.propagate kernels.py:134-165, Sequential kernels.py:184-187, Sum/Mixture
+// kernels.py:220-254.  The host (cnn_gp/netplan.py) lowers the module tree into a list
+// of cgp_net_op over LDS slots; this file only executes the list.
+//
+// Per pair, per conv: a row pass writes horizontal window sums of every input row into
+// the row-sum scratch `hs` ([HSR][WO]; rows outside the input are zero), then a column
+// pass finishes the windows for R3 output rows per item, applies w·Σ + b, the ReLU (with
+// variances prefetched before the row pass) and the residual add, and writes the output
+// slot.  Geometry is compile time (one instantiation per conv shape the reference
+// configs use), so every LDS offset inside a pass is an immediate.
+
+#include "cgp_common.h"
+
+#include <algorithm>
+#include <climits>
+
+using namespace cgp;
+
+namespace {
+
+constexpr int kNT = 128;        // threads per workgroup: two waves per pair
+constexpr int kST = 8;          // supertile edge: pairs are walked in 8x8 (i, j) blocks
+constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
+
+// R | len outputs per item, chosen to minimise rounds·(per-item cost) with ≤ 8 outputs
+// (register budget); ties go to the larger R (fewer LDS reads per output).
+constexpr int pick_r(int lines, int len, int taps, int s, int epi) {
+    int best = 1;
+    long long best_cost = LLONG_MAX;
+    for (int r = 1; r <= 8 && r <= len; ++r) {
+        if (len % r) continue;
+        const int items = lines * (len / r);
+        const int rounds = (items + kNT - 1) / kNT;
+        const long long cost = (long long)rounds * (epi * r + (r - 1) * s + taps);
+        if (cost < best_cost || (cost == best_cost && r > best)) {
+            best = r;
+            best_cost = cost;
+        }
+    }
+    return best;
+}
+
+template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_>
+struct NG {
+    static constexpr int H = H_, W = W_, HO = HO_, WO = WO_, TAPS = TAPS_, S = S_, OFF = OFF_;
+    static constexpr int HW = H * W, HOWO = HO * WO;
+    static constexpr bool POINT = TAPS == 1 && OFF == 0;
+    static constexpr bool REDUCE = HO == 1 && WO == 1 && OFF == 0 && TAPS == H && TAPS == W;
+    static constexpr int HSR = (HO - 1) * S + TAPS;           // hs rows; row q <-> input q+OFF
+    static constexpr int Q0 = OFF < 0 ? -OFF : 0;              // first hs row backed by input
+    static constexpr int Q1 = HSR < H - OFF ? HSR : H - OFF;   // one past the last
+    static constexpr int NVR = Q1 - Q0;                        // input rows the row pass reads
+    static constexpr int R2 = pick_r(NVR, WO, TAPS, S, 2);
+    static constexpr int R3 = pick_r(WO, HO, TAPS, S, 8);
+    static constexpr int WIN2 = (R2 - 1) * S + TAPS, WIN3 = (R3 - 1) * S + TAPS;
+    static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NH + kNT - 1) / kNT;
+    static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NV + kNT - 1) / kNT;
+    static constexpr int NZ = (HSR - NVR) * WO;                // zero cells of hs
+    static constexpr int HS_ELEMS = (POINT || REDUCE) ? 2 : HSR * WO;
+};
+
+// The fused kernel's conv shapes: (H, W, HO, WO, taps, stride, offset) — every conv of the
+// reference configs plus their CIFAR-size analogues.
+#define CGP_NET_GEOMETRIES(X)          \
+    X(28, 28, 28, 28, 7, 1, -3)        \
+    X(28, 28, 28, 28, 4, 1, -1)        \
+    X(28, 28, 28, 28, 3, 1, -1)        \
+    X(28, 28, 28, 28, 1, 1, 0)         \
+    X(28, 28, 14, 14, 3, 2, -1)        \
+    X(28, 28, 14, 14, 1, 2, 0)         \
+    X(28, 28, 1, 1, 28, 1, 0)          \
+    X(14, 14, 14, 14, 3, 1, -1)        \
+    X(14, 14, 7, 7, 3, 2, -1)          \
+    X(14, 14, 7, 7, 1, 2, 0)           \
+    X(7, 7, 7, 7, 3, 1, -1)            \
+    X(7, 7, 1, 1, 7, 1, 0)             \
+    X(1, 1, 1, 1, 1, 1, 0)             \
+    X(32, 32, 32, 32, 3, 1, -1)        \
+    X(32, 32, 32, 32, 1, 1, 0)         \
+    X(32, 32, 16, 16, 3, 2, -1)        \
+    X(32, 32, 16, 16, 1, 2, 0)         \
+    X(16, 16, 16, 16, 3, 1, -1)        \
+    X(16, 16, 8, 8, 3, 2, -1)          \
+    X(16, 16, 8, 8, 1, 2, 0)           \
+    X(8, 8, 8, 8, 3, 1, -1)            \
+    X(8, 8, 1, 1, 8, 1, 0)
+
+struct GeoRow {
+    int h, w, ho, wo, taps, s, off, hs_elems;
+};
+#define CGP_NET_ROW(h, w, ho, wo, k, s, o) {h, w, ho, wo, k, s, o, NG<h, w, ho, wo, k, s, o>::HS_ELEMS},
+constexpr GeoRow kGeoTable[] = {CGP_NET_GEOMETRIES(CGP_NET_ROW)};
+#undef CGP_NET_ROW
+constexpr int kNumGeo = sizeof(kGeoTable) / sizeof(kGeoTable[0]);
+
+// out[o] = Σ_{t<TAPS} w[o·S + t], o < R.  Stride 1 with TAPS ≥ 4: outputs in groups of
+// g ≤ TAPS share the common core of their windows; the left parts are suffix sums and
+// the right parts prefix sums, so a group costs TAPS + 3g - 6 adds instead of g(TAPS-1).
+template <typename T, int TAPS, int O0, int G, int N, int R>
+__device__ __forceinline__ void win_group(const T (&w)[N], T (&out)[R]) {
+    T core = w[O0 + G - 1];
+#pragma unroll
+    for (int t = O0 + G; t < O0 + TAPS; ++t) core += w[t];
+    if constexpr (G == 1) {
+        out[O0] = core;
+    } else {
+        T left[G], right[G];
+        left[G - 2] = w[O0 + G - 2];
+#pragma unroll
+        for (int o = G - 3; o >= 0; --o) left[o] = w[O0 + o] + left[o + 1];
+        right[1] = w[O0 + TAPS];
+#pragma unroll
+        for (int o = 2; o < G; ++o) right[o] = right[o - 1] + w[O0 + TAPS + o - 1];
+        out[O0] = left[0] + core;
+#pragma unroll
+        for (int o = 1; o < G - 1; ++o) out[O0 + o] = (left[o] + core) + right[o];
+        out[O0 + G - 1] = core + right[G - 1];
+    }
+}
+
+template <typename T, int TAPS, int O0, int N, int R>
+__device__ __forceinline__ void win_groups(const T (&w)[N], T (&out)[R]) {
+    if constexpr (O0 < R) {
+        constexpr int G = (R - O0) < TAPS ? (R - O0) : TAPS;
+        win_group<T, TAPS, O0, G, N, R>(w, out);
+        win_groups<T, TAPS, O0 + TAPS, N, R>(w, out);
+    }
+}
+
+template <typename T, int TAPS, int S, int R>
+__device__ __forceinline__ void win_sums(const T (&w)[(R - 1) * S + TAPS], T (&out)[R]) {
+    if constexpr (S == 1 && TAPS >= 4 && R > 1) {
+        win_groups<T, TAPS, 0, (R - 1) * S + TAPS, R>(w, out);
+    } else {
+#pragma unroll
+        for (int o = 0; o < R; ++o) {
+            T acc = w[o * S];
+#pragma unroll
+            for (int t = 1; t < TAPS; ++t) acc += w[o * S + t];
+            out[o] = acc;
+        }
+    }
+}
+
+// threadIdx.x through an opaque move: per-thread index math of one op is then recomputed
+// inside the op instead of being hoisted out of the pair loop, where it would hold
+// registers for every geometry at once
+__device__ __forceinline__ int opaque_tid() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    return t;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+template <typename T>
+struct NetP {
+    const T* __restrict__ x;
+    const T* __restrict__ y;
+    T* __restrict__ out;
+    const T* __restrict__ kdiag;
+    const cgp_net_op* __restrict__ ops;
+    long long ldo, units;
+    unsigned n1, n2, nbi, nbj;
+    int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact;
+};
+
+// EXACT (CGP_FLAG_EXACT_RELU) is a separate instantiation: a call to the out-of-line
+// relu_exact would make every register live across it caller-saved
+template <bool EXACT, typename T>
+__device__ __forceinline__ T relu_of(T c, T v1, T v2) {
+    if constexpr (EXACT)
+        return relu_exact_inl(c, v1, v2);
+    else
+        return relu_fast(c, v1, v2);
+}
+
+// ---- CGP_NET_CONV -------------------------------------------------------------------
+template <typename T, bool EX, class G>
+__device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
+                                         const NetP<T>& p, unsigned i, unsigned j) {
+    const int tid = opaque_tid();
+    const T w = T(op.weight), b = T(op.bias);
+    const bool relu = op.relu != 0, add = op.add >= 0;
+    const T* __restrict__ vx = static_cast<const T*>(op.var_x) + (size_t)i * G::HOWO;
+    const T* __restrict__ vy = static_cast<const T*>(op.var_y) + (size_t)j * G::HOWO;
+    const T* __restrict__ src = lds + op.src;
+    T* __restrict__ dst = lds + op.dst;
+    const T* __restrict__ ad = lds + (add ? op.add : 0);
+    const int wsi = op.ws_in, wso = op.ws_out;
+
+    if constexpr (G::REDUCE) {
+        // 1x1 output from a full-plane window: a block reduction
+        T acc = T(0);
+#pragma unroll
+        for (int k = 0; k < (G::HW + kNT - 1) / kNT; ++k) {
+            const int px = tid + k * kNT;
+            if (G::HW % kNT == 0 || px < G::HW) {
+                const int r = px / G::W, c = px - r * G::W;
+                acc += src[r * wsi + c];
+            }
+        }
+        acc = wave_sum(acc);
+        T* part = lds + p.hs;
+        if ((tid & 63) == 0) part[tid >> 6] = acc;
+        lds_barrier();
+        if (tid == 0) {
+            T v = w * (part[0] + part[1]) + b;
+            if (relu) v = relu_of<EX>(v, vx[0], vy[0]);
+            if (add) v += ad[0];
+            dst[0] = v;
+        }
+    } else if constexpr (G::POINT) {
+        constexpr int KP = (G::HOWO + kNT - 1) / kNT;
+        T v1[KP], v2[KP];
+        if (relu) {
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                const int px = tid + k * kNT;
+                if (G::HOWO % kNT == 0 || px < G::HOWO) {
+                    v1[k] = vx[px];
+                    v2[k] = vy[px];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const int px = tid + k * kNT;
+            if (G::HOWO % kNT == 0 || px < G::HOWO) {
+                const int r = px / G::WO, c = px - r * G::WO;
+                T v = w * src[(r * G::S) * wsi + c * G::S] + b;
+                if (relu) v = relu_of<EX>(v, v1[k], v2[k]);
+                if (add) v += ad[r * wso + c];
+                dst[r * wso + c] = v;
+            }
+        }
+    } else {
+        T* __restrict__ hs = lds + p.hs;
+        // variances of this thread's outputs, in flight during the row pass
+        T v1[G::KV][G::R3], v2[G::KV][G::R3];
+        if (relu) {
+#pragma unroll
+            for (int kv = 0; kv < G::KV; ++kv) {
+                const int it = tid + kv * kNT;
+                if (G::NV % kNT == 0 || it < G::NV) {
+                    const int g3 = it / G::WO, c = it - g3 * G::WO;
+#pragma unroll
+                    for (int k = 0; k < G::R3; ++k) {
+                        v1[kv][k] = vx[(g3 * G::R3 + k) * G::WO + c];
+                        v2[kv][k] = vy[(g3 * G::R3 + k) * G::WO + c];
+                    }
+                }
+            }
+        }
+        // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
+#pragma unroll
+        for (int kh = 0; kh < G::KH; ++kh) {
+            const int it = tid + kh * kNT;
+            if (G::NH % kNT == 0 || it < G::NH) {
+                const int qi = it / G::NG2, g2 = it - qi * G::NG2;
+                const T* row = src + (G::Q0 + qi + G::OFF) * wsi + g2 * G::R2 * G::S + G::OFF;
+                T win[G::WIN2];
+#pragma unroll
+                for (int t = 0; t < G::WIN2; ++t) win[t] = row[t];
+                T o[G::R2];
+                win_sums<T, G::TAPS, G::S, G::R2>(win, o);
+                T* h = hs + (G::Q0 + qi) * G::WO + g2 * G::R2;
+#pragma unroll
+                for (int t = 0; t < G::R2; ++t) h[t] = o[t];
+            }
+        }
+        // hs rows outside the input are zero (the scratch is shared by every conv)
+        if constexpr (G::NZ > 0) {
+#pragma unroll
+            for (int z0 = 0; z0 < G::NZ; z0 += kNT) {
+                const int z = z0 + tid;
+                if (G::NZ % kNT == 0 || z < G::NZ)
+                    hs[z < G::Q0 * G::WO ? z : z + G::NVR * G::WO] = T(0);
+            }
+        }
+        lds_barrier();
+        // column pass + epilogue
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv) {
+            const int it = tid + kv * kNT;
+            if (G::NV % kNT == 0 || it < G::NV) {
+                const int g3 = it / G::WO, c = it - g3 * G::WO;
+                const T* col = hs + g3 * G::R3 * G::S * G::WO + c;
+                T win[G::WIN3];
+#pragma unroll
+                for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
+                T o[G::R3];
+                win_sums<T, G::TAPS, G::S, G::R3>(win, o);
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k) {
+                    const int r = g3 * G::R3 + k;
+                    T v = w * o[k] + b;
+                    if (relu) v = relu_of<EX>(v, v1[kv][k], v2[kv][k]);
+                    if (add) v += ad[r * wso + c];
+                    dst[r * wso + c] = v;
+                }
+            }
+        }
+    }
+}
+
+// ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
+template <typename T, bool EX, int KIND>
+__device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
+                                         const NetP<T>& p, unsigned i, unsigned j) {
+    const int tid = opaque_tid();
+    const int wd = op.w, hw = op.h * op.w, ws = op.ws_out;
+    const FastDiv fw{op.div_m, op.div_s, (unsigned)op.w};
+    const bool add = op.add >= 0;
+    const T* __restrict__ vx = static_cast<const T*>(op.var_x) + (size_t)i * hw;
+    const T* __restrict__ vy = static_cast<const T*>(op.var_y) + (size_t)j * hw;
+    const T* __restrict__ xi = p.x + (size_t)i * p.channels * hw;
+    const T* __restrict__ yj = p.y + (size_t)j * p.channels * hw;
+    for (int base = 0; base < hw; base += kEw * kNT) {
+        T a[kEw], v1[kEw], v2[kEw];
+#pragma unroll
+        for (int k = 0; k < kEw; ++k) {
+            const int px = base + k * kNT + tid;
+            if (px < hw) {
+                if constexpr (KIND == CGP_NET_RELU) {
+                    v1[k] = vx[px];
+                    v2[k] = vy[px];
+                } else if constexpr (KIND == CGP_NET_MOMENTS) {
+                    T acc = xi[px] * yj[px];
+                    for (int ch = 1; ch < p.channels; ++ch)
+                        acc += xi[(size_t)ch * hw + px] * yj[(size_t)ch * hw + px];
+                    a[k] = acc / T(p.channels);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kEw; ++k) {
+            const int px = base + k * kNT + tid;
+            if (px < hw) {
+                const int r = (int)fdiv((unsigned)px, fw), c = px - r * wd;
+                const int at = r * ws + c;
+                T v;
+                if constexpr (KIND == CGP_NET_RELU) {
+                    v = relu_of<EX>(lds[op.src + at], v1[k], v2[k]);
+                    if (add) v += lds[op.add + at];
+                } else if constexpr (KIND == CGP_NET_LINEAR) {
+                    v = T(op.weight) * lds[op.src + at] + T(op.bias) * lds[op.add + at];
+                } else {
+                    v = a[k];
+                }
+                lds[op.dst + at] = v;
+            }
+        }
+    }
+}
+
+// pair walk: supertile s (8x8 pairs) -> (bi, bj); same tiles enumerate the upper
+// triangle (bi <= bj) row-major
+__device__ __forceinline__ void tri_decode(unsigned s, unsigned nb, unsigned& bi,
+                                           unsigned& bj) {
+    const double a = 2.0 * nb + 1.0;
+    long long r = (long long)((a - sqrt(a * a - 8.0 * (double)s)) * 0.5);
+    auto off = [nb](long long q) { return q * (long long)nb - q * (q - 1) / 2; };
+    if (r < 0) r = 0;
+    while (r > 0 && off(r) > (long long)s) --r;
+    while (off(r + 1) <= (long long)s) ++r;
+    bi = (unsigned)r;
+    bj = (unsigned)(r + ((long long)s - off(r)));
+}
+
+constexpr int geo_index(int h, int w, int ho, int wo, int k, int s, int o) {
+    for (int n = 0; n < kNumGeo; ++n) {
+        const GeoRow& g = kGeoTable[n];
+        if (g.h == h && g.w == w && g.ho == ho && g.wo == wo && g.taps == k && g.s == s &&
+            g.off == o)
+            return n;
+    }
+    return -1;
+}
+
+#define CGP_NET_CASE(h, w, ho, wo, k, s, o)                                          \
+    case geo_index(h, w, ho, wo, k, s, o):                                           \
+        net_conv<T, EX, NG<h, w, ho, wo, k, s, o>>(lds, op, p, i, j);                    \
+        break;
+
+template <typename T, bool EX>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void net_kernel(const NetP<T> p) {
+    extern __shared__ __align__(16) unsigned char smem_raw[];
+    T* lds = reinterpret_cast<T*>(smem_raw);
+    const int tid = threadIdx.x;
+    for (int e = tid; e < p.lds_elems; e += kNT) lds[e] = T(0);   // slot halos stay zero
+    lds_barrier();
+    // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
+    // contiguous run of supertiles and its L2 holds the images/variances they share
+    const unsigned g8 = gridDim.x / 8, xcd = blockIdx.x % 8, l = blockIdx.x / 8;
+    const long long per = (p.units + 7) / 8;
+    const long long beg = (long long)xcd * per;
+    const long long end = beg + per < p.units ? beg + per : p.units;
+    for (long long u = beg + l; u < end; u += g8) {
+        const unsigned s = (unsigned)(u >> 6), q = (unsigned)u & 63u;
+        unsigned bi, bj;
+        if (p.same) {
+            tri_decode(s, p.nbi, bi, bj);
+        } else {
+            bi = s / p.nbj;
+            bj = s - bi * p.nbj;
+        }
+        const unsigned i = bi * kST + (q >> 3), j = bj * kST + (q & 7u);
+        if (i >= p.n1 || j >= p.n2) continue;
+        if (p.same && j <= i) {
+            if (j == i && tid == 0) p.out[(long long)i * p.ldo + i] = p.kdiag[i];
+            continue;
+        }
+        for (int k = 0; k < p.nops; ++k) {
+            const cgp_net_op op = p.ops[k];
+            switch (op.kind) {
+            case CGP_NET_CONV:
+                switch (op.code) {
+                    CGP_NET_GEOMETRIES(CGP_NET_CASE)
+                default:
+                    break;
+                }
+                break;
+            case CGP_NET_RELU:
+                net_elem<T, EX, CGP_NET_RELU>(lds, op, p, i, j);
+                break;
+            case CGP_NET_MOMENTS:
+                net_elem<T, EX, CGP_NET_MOMENTS>(lds, op, p, i, j);
+                break;
+            case CGP_NET_LINEAR:
+                net_elem<T, EX, CGP_NET_LINEAR>(lds, op, p, i, j);
+                break;
+            default:
+                break;
+            }
+            lds_barrier();
+        }
+        if (tid == 0) {
+            const T v = lds[p.final_slot];
+            p.out[(long long)i * p.ldo + j] = v;
+            if (p.same) p.out[(long long)j * p.ldo + i] = v;
+        }
+        lds_barrier();
+    }
+}
+
+template <typename T, bool EX>
+int net_occupancy(int lds_bytes) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, net_kernel<T, EX>, kNT, lds_bytes) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+template <typename T>
+int net_impl(const cgp_net_args* a, void* stream) {
+    if (!a) return fail(CGP_EINVAL, "net: args is NULL");
+    if (!a->x || !a->y || !a->out || !a->ops || a->nops <= 0)
+        return fail(CGP_EINVAL, "net: NULL pointer or empty op list");
+    if (a->n1 <= 0 || a->n2 <= 0 || a->n1 >= (1LL << 31) || a->n2 >= (1LL << 31) ||
+        a->ldo < a->n2)
+        return fail(CGP_EINVAL, "net: bad sizes n1=%lld n2=%lld ldo=%lld", (long long)a->n1,
+                    (long long)a->n2, (long long)a->ldo);
+    if (a->same && (a->n1 != a->n2 || !a->kdiag))
+        return fail(CGP_EINVAL, "net: same tile needs n1 == n2 and kdiag");
+    if (a->channels <= 0 || a->h <= 0 || a->w <= 0)
+        return fail(CGP_EINVAL, "net: bad image shape");
+    const long long lds_bytes = (long long)a->lds_elems * (long long)sizeof(T);
+    if (a->lds_elems <= 0 || lds_bytes > 160 * 1024)
+        return fail(CGP_EINVAL, "net: LDS footprint %lld bytes out of range", lds_bytes);
+    if (a->final_slot < 0 || a->final_slot >= a->lds_elems || a->hs < 0 ||
+        a->hs >= a->lds_elems)
+        return fail(CGP_EINVAL, "net: slot offsets out of range");
+    NetP<T> p;
+    p.x = static_cast<const T*>(a->x);
+    p.y = static_cast<const T*>(a->y);
+    p.out = static_cast<T*>(a->out);
+    p.kdiag = static_cast<const T*>(a->kdiag);
+    p.ops = a->ops;
+    p.ldo = a->ldo;
+    p.n1 = (unsigned)a->n1;
+    p.n2 = (unsigned)a->n2;
+    p.nbi = (unsigned)((a->n1 + kST - 1) / kST);
+    p.nbj = (unsigned)((a->n2 + kST - 1) / kST);
+    const long long tiles = a->same ? (long long)p.nbi * (p.nbi + 1) / 2
+                                    : (long long)p.nbi * p.nbj;
+    if (tiles * 64 >= (1LL << 40)) return fail(CGP_EINVAL, "net: tile too large");
+    p.units = tiles * 64;
+    p.nops = a->nops;
+    p.channels = a->channels;
+    p.hw_in = a->h * a->w;
+    p.same = a->same;
+    p.final_slot = a->final_slot;
+    p.hs = a->hs;
+    p.lds_elems = a->lds_elems;
+    p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
+    const void* fn = p.exact ? reinterpret_cast<const void*>(net_kernel<T, true>)
+                             : reinterpret_cast<const void*>(net_kernel<T, false>);
+    if (lds_bytes > 64 * 1024)
+        CGP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_bytes));
+    const int per_cu = p.exact ? net_occupancy<T, true>((int)lds_bytes)
+                               : net_occupancy<T, false>((int)lds_bytes);
+    if (per_cu <= 0) return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS",
+                                 lds_bytes);
+    long long grid = (long long)per_cu * device_cus();
+    if (grid > p.units) grid = p.units;
+    grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
+    if (p.exact)
+        hipLaunchKernelGGL((net_kernel<T, true>), dim3((unsigned)grid), dim3(kNT),
+                           (size_t)lds_bytes, as_stream(stream), p);
+    else
+        hipLaunchKernelGGL((net_kernel<T, false>), dim3((unsigned)grid), dim3(kNT),
+                           (size_t)lds_bytes, as_stream(stream), p);
+    return check_launch("net_kernel");
+}
+
+}  // namespace
+
+extern "C" {
+
+int cgp_net_geometry(int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t taps,
+                     int32_t stride, int32_t offset) {
+    for (int k = 0; k < kNumGeo; ++k) {
+        const GeoRow& g = kGeoTable[k];
+        if (g.h == h && g.w == w && g.ho == ho && g.wo == wo && g.taps == taps &&
+            g.s == stride && g.off == offset)
+            return k;
+    }
+    return -1;
+}
+
+size_t cgp_net_op_size(void) { return sizeof(cgp_net_op); }
+size_t cgp_net_args_size(void) { return sizeof(cgp_net_args); }
+
+int cgp_net_hs_elems(int32_t code) {
+    return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;
+}
+
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64) {
+    if (lds_bytes <= 0 || lds_bytes > 160 * 1024) return 0;
+    if (lds_bytes > 64 * 1024) {
+        const void* fn = f64 ? reinterpret_cast<const void*>(net_kernel<double, false>)
+                             : reinterpret_cast<const void*>(net_kernel<float, false>);
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
+    }
+    return f64 ? net_occupancy<double, false>(lds_bytes) : net_occupancy<float, false>(lds_bytes);
+}
+
+int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }
+int cgp_net_f32(const cgp_net_args* args, void* stream) { return net_impl<float>(args, stream); }
+
+}  // extern "C"

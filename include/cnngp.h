@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 2
+#define CGP_ABI_VERSION 3
 
 /* error codes */
 #define CGP_OK 0
@@ -190,6 +190,73 @@ int cgp_gemm_f64(const double* a, const double* b, double* c, int64_t m, int64_t
 /* out[r] = argmax_c a[r][c] (first maximum, like torch.argmax), a: [rows][cols] */
 int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* out,
                         void* stream);
+
+
+/* ---------------------------------------------------------------------------------
+ * Whole-network pair kernel.  Replaces the per-layer loop of Sequential.propagate
+ * (kernels.py:184-187) over ALL layers for a tile: one workgroup owns one (i, j) pair
+ * at a time and carries its covariance map through every op in LDS; only the images,
+ * the per-image variance maps (read-only, L2-resident) and the final K[i, j] touch
+ * global memory.  The host lowers the module tree to a list of cgp_net_op over LDS
+ * "slots" (row-major planes with zero column halos) and supplies the
+ * variance maps from the per-image pipeline (cgp_conv_* / cgp_var_relu_* on xx, yy).
+ *
+ *   CGP_NET_MOMENTS  dst = mean_c x_i[c]·y_j[c]                   kernels.py:44-47
+ *   CGP_NET_CONV     dst = w·Σ_window src + b  [→ ReLU] [+ add]    kernels.py:92-98
+ *   CGP_NET_RELU     dst = relu(src)           [+ add]            kernels.py:134-165
+ *   CGP_NET_LINEAR   dst = weight·src + bias·add   (Sum / Mixture: kernels.py:220-254)
+ *
+ * Same tiles (same=1) evaluate only i < j, mirror K[j, i] = K[i, j] (the recursion is
+ * symmetric in (i, j) when y = x) and take K[i, i] = kdiag[i] — the per-image
+ * pipeline's final value, which is exactly what the reference's same/diag override of
+ * every ReLU (kernels.py:155-162) makes the (i, i) pair map equal to.
+ * --------------------------------------------------------------------------------- */
+#define CGP_NET_CONV 0
+#define CGP_NET_RELU 1
+#define CGP_NET_MOMENTS 2
+#define CGP_NET_LINEAR 3
+
+typedef struct cgp_net_op {
+    int32_t kind;          /* CGP_NET_* */
+    int32_t code;          /* CONV: cgp_net_geometry() of the conv */
+    int32_t src, dst, add; /* LDS element offsets of the slots' (0, 0) pixel; add < 0: none */
+    int32_t ws_in, ws_out; /* row strides (elements) of the src slot / dst and add slots */
+    int32_t relu;          /* CONV: apply the ReLU map to the conv output (then + add) */
+    int32_t h, w;          /* RELU / LINEAR / MOMENTS: map size (CONV: output size) */
+    uint32_t div_m, div_s; /* w as a multiply-high divisor (host: make_fastdiv(w)) */
+    double weight, bias;   /* CONV: w·Σ + b;  LINEAR: dst = weight·src + bias·add */
+    const void* var_x;     /* ReLU input variances of the x images, [n1][h·w] */
+    const void* var_y;     /* ... of the y images, [n2][h·w] */
+} cgp_net_op;
+
+typedef struct cgp_net_args {
+    const void* x;         /* images [n1][channels][h][w] */
+    const void* y;         /* images [n2][channels][h][w] (== x when same) */
+    void* out;             /* K tile [n1][ldo] */
+    const void* kdiag;     /* same tiles: K[i, i] (the per-image final variance), [n1] */
+    const cgp_net_op* ops; /* DEVICE array of nops ops */
+    int64_t n1, n2, ldo;
+    int32_t nops, channels, h, w;
+    int32_t same;          /* 1: y is x (Kxx diagonal tile) */
+    int32_t final_slot;    /* LDS offset of the 1x1 result */
+    int32_t hs;            /* LDS offset of the row-sum scratch */
+    int32_t lds_elems;     /* LDS footprint (elements of the compute type) */
+    int32_t flags;         /* CGP_FLAG_EXACT_RELU */
+    int32_t reserved;
+} cgp_net_args;
+
+/* Geometry code of a conv for CGP_NET_CONV, or -1 if the fused kernel has no
+ * instantiation for it (the caller then runs the layer-by-layer path). */
+int cgp_net_geometry(int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t taps,
+                     int32_t stride, int32_t offset);
+/* elements of row-sum scratch the conv of geometry `code` needs (-1: bad code) */
+int cgp_net_hs_elems(int32_t code);
+size_t cgp_net_op_size(void);
+size_t cgp_net_args_size(void);
+/* workgroups per CU the fused kernel reaches with lds_bytes of LDS (0 if it cannot run) */
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64);
+int cgp_net_f64(const cgp_net_args* args, void* stream);
+int cgp_net_f32(const cgp_net_args* args, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,133 @@
+"""CPU emulator of the whole-network kernel's op list (test infrastructure only).
+
+Executes ``NetPlan.records`` exactly as csrc/netfuse.hip does — one flat LDS array per
+pair, slots at the planned offsets, zero halos, row-sum scratch with zero rows — so the
+host lowering (slot classes, halos, in-place reuse, LINEAR chains) is checked against the
+oracle without a GPU.  Variances come from a plain numpy run of the same SSA program on
+the per-image maps.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from oracle import nngp_oracle as O
+
+TINY = O.F32_TINY
+
+
+def _conv_maps(m, geom, weight, bias):
+    """Direct window sums on [n, H, W] maps: w·Σ_window + b with zero padding."""
+    h, w, ho, wo, taps, s, off = geom
+    n = m.shape[0]
+    out = np.zeros((n, ho, wo), m.dtype)
+    for r in range(ho):
+        for c in range(wo):
+            acc = np.zeros(n, m.dtype)
+            for a in range(taps):
+                rr = r * s + off + a
+                if not 0 <= rr < h:
+                    continue
+                for b in range(taps):
+                    cc = c * s + off + b
+                    if 0 <= cc < w:
+                        acc = acc + m[:, rr, cc]
+            out[:, r, c] = weight * acc + bias
+    return out
+
+
+def variances(plan, x, y):
+    """value -> (xx [n1,H,W], yy [n2,H,W]) for every value of the program."""
+    C = x.shape[1]
+    vals = {plan.v0: ((x * x).sum(1) / C, (y * y).sum(1) / C)}
+    for op in plan.prog.ops:
+        if op.kind == "conv":
+            g = op.geom
+            geom = (*op.shape_in, *op.shape_out, g.taps, g.stride, g.offset)
+            vals[op.dst] = tuple(_conv_maps(m, geom, g.weight, g.bias) for m in vals[op.src])
+        elif op.kind == "relu":
+            vals[op.dst] = tuple(m / 2 for m in vals[op.src])
+        else:
+            acc = None
+            for coef, t in op.terms:
+                a = vals[t] if coef is None else tuple(m * coef for m in vals[t])
+                acc = a if acc is None else (acc[0] + a[0], acc[1] + a[1])
+            vals[op.dst] = acc
+    return vals
+
+
+def _relu(c, v1, v2):
+    with np.errstate(invalid="ignore", divide="ignore"):
+        t = v1 * v2 + TINY
+        cos = np.clip(c * (1.0 / np.sqrt(t)), -1.0, 1.0)
+        sin = np.sqrt(np.maximum(t - c * c, 0.0))
+        return (sin + (math.pi - np.arccos(cos)) * c) / (2 * math.pi)
+
+
+def run_pair(net, x_i, y_j, var, i, j):
+    lds = np.zeros(net.lds_elems)
+    hs0 = net.hs
+
+    def plane(off, h, w, ws):
+        idx = off + np.arange(h)[:, None] * ws + np.arange(w)[None, :]
+        return idx
+
+    for f, v in net.records:
+        kind = f["kind"]
+        if kind == 2:                                           # MOMENTS
+            h, w = f["h"], f["w"]
+            C = x_i.shape[0]
+            lds[plane(f["dst"], h, w, f["ws_out"])] = (x_i * y_j).sum(0) / C
+        elif kind == 0:                                         # CONV
+            h, w, ho, wo, taps, s, off = f["geom"]
+            src = lds[plane(f["src"], h, w, f["ws_in"])]
+            # row pass over the planned slot (reads the halo columns from `lds`)
+            hsr = (ho - 1) * s + taps
+            hs = np.zeros((hsr, wo))
+            for q in range(hsr):
+                r = q + off
+                if not 0 <= r < h:
+                    continue
+                for c in range(wo):
+                    base = f["src"] + r * f["ws_in"] + c * s + off
+                    hs[q, c] = lds[base:base + taps].sum()
+            out = np.zeros((ho, wo))
+            for r in range(ho):
+                out[r] = hs[r * s:r * s + taps].sum(0)
+            out = f["weight"] * out + f["bias"]
+            if f.get("relu"):
+                vx, vy = var[v]
+                out = _relu(out, vx[i], vy[j])
+            if f["add"] >= 0:
+                out = out + lds[plane(f["add"], ho, wo, f["ws_out"])]
+            lds[plane(f["dst"], ho, wo, f["ws_out"])] = out
+            lds[hs0:hs0 + 2] = 0.0
+        elif kind == 1:                                         # RELU
+            h, w = f["h"], f["w"]
+            vx, vy = var[v]
+            out = _relu(lds[plane(f["src"], h, w, f["ws_in"])], vx[i], vy[j])
+            if f["add"] >= 0:
+                out = out + lds[plane(f["add"], h, w, f["ws_out"])]
+            lds[plane(f["dst"], h, w, f["ws_out"])] = out
+        else:                                                   # LINEAR
+            h, w = f["h"], f["w"]
+            out = f["weight"] * lds[plane(f["src"], h, w, f["ws_in"])] + \
+                f["bias"] * lds[plane(f["add"], h, w, f["ws_out"])]
+            lds[plane(f["dst"], h, w, f["ws_out"])] = out
+    return lds[net.final_slot]
+
+
+def kernel(net, x, y, same):
+    var = variances(net.plan, x, y)
+    n1, n2 = x.shape[0], y.shape[0]
+    K = np.zeros((n1, n2))
+    for i in range(n1):
+        for j in range(n2):
+            if same and i == j:
+                K[i, i] = var[net.plan.vf][0][i].item()
+            elif same and j < i:
+                K[i, j] = K[j, i]
+            else:
+                K[i, j] = run_pair(net, x[i], y[j], var, i, j)
+    return K

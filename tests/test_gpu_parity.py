@@ -292,16 +292,83 @@ def test_e2e_matches_reference_golden(cfg, dtn, numerics):
 
 @pytest.mark.parametrize("cfg", CFGS)
 def test_fusion_is_exact(cfg):
-    """the fused program and the op-by-op program give identical results"""
+    """layer path: the fused program and the op-by-op program give identical results"""
     rng = np.random.default_rng(3)
     C, side = specs.GEOMETRY[cfg]
     X = dev(rng.random((5, C, side, side)))
     Z = dev(rng.random((3, C, side, side)))
-    m = configs_util.model(cfg).to(DEV, torch.float64)
+    m = configs_util.model(cfg).to(DEV, torch.float64).set_fused_network(False)
     with torch.no_grad():
         a = m(X, Z, False, False).cpu().numpy()
         b = m.set_fusion(False)(X, Z, False, False).cpu().numpy()
     assert rel_err(a, b) < 1e-13
+
+
+# ------------------------------------------------------------------------------------
+# whole-network kernel (csrc/netfuse.hip) against the layer path and the oracle
+# ------------------------------------------------------------------------------------
+def _uses_net(m, side, itemsize):
+    plan = m._plan(side, side)
+    return m._net_plan(plan, itemsize) is not None
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("dtn", ["f64", "f32"])
+@pytest.mark.parametrize("same", [True, False])
+def test_netfuse_matches_layer_path(cfg, dtn, same):
+    """the two device paths evaluate the same recursion (different summation orders):
+    fp64 within 1e-12, fp32 within 2e-5"""
+    rng = np.random.default_rng(11)
+    C, side = specs.GEOMETRY[cfg]
+    tdt = torch.float64 if dtn == "f64" else torch.float32
+    X = dev(rng.random((13, C, side, side)), tdt)
+    Z = dev(rng.random((10, C, side, side)), tdt)
+    m = configs_util.model(cfg).to(DEV, tdt)
+    assert _uses_net(m, side, X.element_size())
+    with torch.no_grad():
+        a = (m(X) if same else m(X, Z, False, False)).cpu().numpy()
+        m.set_fused_network(False)
+        b = (m(X) if same else m(X, Z, False, False)).cpu().numpy()
+    assert rel_err(a, b) < (1e-12 if dtn == "f64" else RTOL32)
+    if same:
+        assert np.array_equal(a, a.T)
+
+
+@pytest.mark.parametrize("n1,n2", [(1, 1), (1, 9), (9, 1), (7, 17), (17, 8), (8, 8)])
+def test_netfuse_ragged_tiles_vs_oracle(n1, n2):
+    """supertile walk: sizes that are not multiples of the 8x8 pair block"""
+    spec = specs.mnist_paper_residual_cnn_gp()
+    m = configs_util.model("mnist_paper_residual_cnn_gp").double().to(DEV)
+    rng = np.random.default_rng(n1 * 100 + n2)
+    X = rng.random((n1, 1, 28, 28))
+    Z = rng.random((n2, 1, 28, 28))
+    got = m(dev(X), dev(Z), False, False).cpu().numpy()
+    assert rel_err(got, O.kernel(spec, X, Z, False, False)) < RTOL64["fast"]
+    gxx = m(dev(Z)).cpu().numpy()
+    assert rel_err(gxx, O.kernel(spec, Z)) < RTOL64["fast"]
+
+
+def test_netfuse_mixture_and_multiterm_sum():
+    """LINEAR ops: a 3-branch Mixture and a 3-term Sum at 28x28 (fused geometries)"""
+    spec_m = cnn_gp.Sequential(
+        cnn_gp.Conv2d(3, var_bias=0.3),
+        cnn_gp.Mixture([cnn_gp.Sequential(),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3, var_weight=2.0)),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(7))],
+                       torch.tensor([0.3, -0.2, 0.1])),
+        cnn_gp.Sum([cnn_gp.Sequential(), cnn_gp.ReLU(),
+                    cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(1, var_bias=0.5))]),
+        cnn_gp.ReLU(), cnn_gp.Conv2d(28, padding=0))
+    rng = np.random.default_rng(8)
+    X = rng.random((5, 1, 28, 28))
+    Z = rng.random((3, 1, 28, 28))
+    m = spec_m.double().to(DEV)
+    assert _uses_net(m, 28, 8)
+    ref = O.kernel(configs_util.spec_of(spec_m), X, Z, False, False)
+    got = m(dev(X), dev(Z), False, False).cpu().numpy()
+    assert rel_err(got, ref) < 1e-6     # softmax: torch (product) vs numpy (oracle)
+    lay = m.set_fused_network(False)(dev(X), dev(Z), False, False).cpu().numpy()
+    assert rel_err(got, lay) < 1e-12
 
 
 def test_cpu_inputs_round_trip_to_host():

@@ -1,0 +1,72 @@
+"""Whole-network kernel lowering (cnn_gp/netplan.py) checked on CPU: the op list, run by a
+numpy emulator of csrc/netfuse.hip (tests/net_emulator.py) over the planned LDS slots,
+must reproduce the oracle — this pins slot classes, halos, in-place reuse and LINEAR
+chains without a GPU."""
+import numpy as np
+import pytest
+import torch
+
+import cnn_gp
+import configs_util
+import net_emulator as E
+from cnn_gp.netplan import NetPlan, Unsupported
+from cnn_gp.program import Plan
+from oracle import nngp_oracle as O
+from oracle import specs
+
+
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp",
+                                 "mnist_as_tf", "cifar10"])
+def test_emulated_net_program_matches_oracle(cfg):
+    C, side = specs.GEOMETRY[cfg]
+    m = configs_util.model(cfg)
+    net = NetPlan(Plan(m, side, side))
+    rng = np.random.default_rng(5)
+    X = rng.random((3, C, side, side))
+    Z = rng.random((2, C, side, side))
+    spec = configs_util.spec_of(m)
+    np.testing.assert_allclose(E.kernel(net, X, X, True), O.kernel(spec, X), rtol=1e-13)
+    np.testing.assert_allclose(E.kernel(net, X, Z, False), O.kernel(spec, X, Z, False),
+                               rtol=1e-13)
+    assert net.lds_elems * 8 <= 48 * 1024      # ≥ 3 workgroups per CU
+
+
+def test_emulated_mixture_and_multiterm_sum():
+    m = cnn_gp.Sequential(
+        cnn_gp.Conv2d(3, var_bias=0.3),
+        cnn_gp.Mixture([cnn_gp.Sequential(),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3, var_weight=2.0)),
+                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(7))],
+                       torch.tensor([0.3, -0.2, 0.1])),
+        cnn_gp.Sum([cnn_gp.Sequential(), cnn_gp.ReLU(),
+                    cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(1, var_bias=0.5))]),
+        cnn_gp.ReLU(), cnn_gp.Conv2d(28, padding=0))
+    net = NetPlan(Plan(m, 28, 28))
+    kinds = [f["kind"] for f, _ in net.records]
+    assert kinds.count(3) >= 3                 # LINEAR chain
+    rng = np.random.default_rng(6)
+    X = rng.random((3, 1, 28, 28))
+    Z = rng.random((2, 1, 28, 28))
+    ref = O.kernel(configs_util.spec_of(m), X, Z, False, False)
+    np.testing.assert_allclose(E.kernel(net, X, Z, False), ref, rtol=1e-6)
+
+
+def test_unsupported_programs_fall_back():
+    with pytest.raises(Unsupported):           # geometry without an instantiation
+        NetPlan(Plan(cnn_gp.Sequential(cnn_gp.Conv2d(3), cnn_gp.ReLU(),
+                                       cnn_gp.Conv2d(10, padding=0)), 10, 10))
+    with pytest.raises(Unsupported):           # output map is not 1x1
+        NetPlan(Plan(cnn_gp.Sequential(cnn_gp.Conv2d(3)), 28, 28))
+    with pytest.raises(Unsupported):           # dilation
+        NetPlan(Plan(cnn_gp.Sequential(cnn_gp.Conv2d(3, dilation=2), cnn_gp.ReLU(),
+                                       cnn_gp.Conv2d(28, padding=0)), 28, 28))
+
+
+def test_slot_reuse_is_tight():
+    """ResNet: two 28x28 slots suffice (block input + branch, branch convs in place)"""
+    net = NetPlan(Plan(configs_util.model("mnist_as_tf"), 28, 28))
+    ws = net.ws[(28, 28)]
+    n28 = len({f["dst"] for f, _ in net.records if f["h"] == 28 and f["kind"] != 0
+               or f["kind"] == 0 and f.get("geom", (0,) * 7)[2] == 28})
+    assert n28 <= 3
+    assert ws == 30
