@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("CNNGP_LIB",
 CGP_ABI_VERSION = 3
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
+CGP_FLAG_NET_DUAL = 4
 CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
 CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
@@ -56,7 +57,9 @@ class NetOp(ctypes.Structure):
         ("kind", _i32), ("code", _i32), ("src", _i32), ("dst", _i32), ("add", _i32),
         ("ws_in", _i32), ("ws_out", _i32), ("relu", _i32), ("h", _i32), ("w", _i32),
         ("div_m", ctypes.c_uint32), ("div_s", ctypes.c_uint32),
+        ("dst2", _i32), ("reserved", _i32),
         ("weight", _f64), ("bias", _f64), ("var_x", _vp), ("var_y", _vp),
+        ("var2_x", _vp), ("var2_y", _vp),
     ]
 
 
@@ -108,9 +111,10 @@ SIGNATURES = {
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_net_geometry": (_i32, [_i32] * 7),
     "cgp_net_hs_elems": (_i32, [_i32]),
+    "cgp_net_resolution": (_i32, [_i32, _i32]),
     "cgp_net_op_size": (ctypes.c_size_t, []),
     "cgp_net_args_size": (ctypes.c_size_t, []),
-    "cgp_net_occupancy": (_i32, [_i32, _i32]),
+    "cgp_net_occupancy": (_i32, [_i32, _i32, _i32]),
     "cgp_net_f64": (_i32, [ctypes.POINTER(NetArgs), _vp]),
     "cgp_net_f32": (_i32, [ctypes.POINTER(NetArgs), _vp]),
 }

@@ -61,7 +61,7 @@ def _conv_halo(op):
 class NetPlan:
     """The whole-network kernel program for one Plan (one model at one input size)."""
 
-    def __init__(self, plan, itemsize: int = 8):
+    def __init__(self, plan, itemsize: int = 8, dual: bool = True):
         self.plan = plan
         prog, v0, vf = plan.prog, plan.v0, plan.vf
         if plan.final_hw != (1, 1):
@@ -196,11 +196,34 @@ class NetPlan:
                     for (c, _), so in zip(terms[2:], srcs[2:]):
                         recs.append((dict(base, src=d.origin, add=so, weight=1.0, bias=c),
                                      None))
+        # 5. dual outputs: a standalone ReLU of the value the previous op just produced
+        #    (a residual block's relu(x) branch input) is written by that op's output
+        #    stage as a second result, saving an op, a barrier and an LDS round trip
+        if dual:
+            folded = []
+            for f, v in recs:
+                prev = folded[-1][0] if folded else None
+                if (f["kind"] == N.CGP_NET_RELU and f["add"] < 0 and prev is not None
+                        and prev["kind"] in (N.CGP_NET_CONV, N.CGP_NET_LINEAR)
+                        and not prev.get("relu") and prev.get("dst2", -1) < 0
+                        and prev["dst"] == f["src"] and (prev["h"], prev["w"]) == (f["h"], f["w"])):
+                    prev["dst2"] = f["dst"]
+                    prev["var2"] = v
+                    continue
+                folded.append((f, v))
+            recs = folded
+        for f, _ in recs:
+            if f["kind"] == N.CGP_NET_RELU:
+                f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
+            elif f["kind"] != N.CGP_NET_CONV:
+                f["code"] = -1
         self.final_slot = slots[vf].origin
         self.hs = 0
         self.lds_elems = top
         self.records = recs
-        self.need_var = {v for _, v in recs if v is not None} | {vf}
+        self.dual = any(f.get("dst2", -1) >= 0 for f, _ in recs)
+        self.need_var = {v for _, v in recs if v is not None} | {vf} | \
+            {f["var2"] for f, _ in recs if "var2" in f}
         self.n_ops = len(recs)
         if self.lds_elems * itemsize > MAX_LDS_BYTES:
             raise Unsupported(f"LDS footprint {self.lds_elems * itemsize} B")
@@ -220,9 +243,13 @@ class NetPlan:
             o.h, o.w = f["h"], f["w"]
             o.div_m, o.div_s = N.make_fastdiv(f["w"])
             o.weight, o.bias = f.get("weight", 0.0), f.get("bias", 0.0)
+            o.dst2 = f.get("dst2", -1)
             if v is not None:
                 vx, vy = var[v]
                 o.var_x, o.var_y = vx.data_ptr(), vy.data_ptr()
+            if "var2" in f:
+                vx, vy = var[f["var2"]]
+                o.var2_x, o.var2_y = vx.data_ptr(), vy.data_ptr()
         return arr
 
     def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
@@ -245,6 +272,6 @@ class NetPlan:
         a.nops, a.channels, a.h, a.w = self.n_ops, x.shape[1], x.shape[2], x.shape[3]
         a.same, a.final_slot, a.hs, a.lds_elems = int(same), self.final_slot, self.hs, \
             self.lds_elems
-        a.flags = flags
+        a.flags = flags | (N.CGP_FLAG_NET_DUAL if self.dual else 0)
         N.check(getattr(N.load(), f"cgp_net_{sfx}")(ctypes.byref(a), stream), "cgp_net")
         return out

@@ -139,6 +139,55 @@ __device__ __forceinline__ float fma_t(float a, float b, float c) {
     return __builtin_fmaf(a, b, c);
 }
 
+// Polynomial coefficients as SGPR operands.  With compile-time constants the compiler
+// pins them in VGPRs and turns every Horner step into v_mov_b64 + v_fmac_f64; read from
+// a __constant__ table through a pointer it cannot hoist (poly_table()), each step is one
+// v_fma_f64 with an SGPR-pair operand and the table lives in SGPRs only while in use.
+static __constant__ double kReluPolyTabD[kReluPolyDegD + 1] = {
+#define CGP_C(k) kReluPolyD[k]
+    CGP_C(0), CGP_C(1), CGP_C(2), CGP_C(3), CGP_C(4), CGP_C(5), CGP_C(6), CGP_C(7),
+    CGP_C(8), CGP_C(9), CGP_C(10), CGP_C(11), CGP_C(12), CGP_C(13), CGP_C(14), CGP_C(15)};
+#undef CGP_C
+static_assert(kReluPolyDegD == 15, "kReluPolyTabD lists 16 coefficients");
+
+typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
+struct PolyTab {
+    ConstD d;
+};
+__device__ __forceinline__ PolyTab poly_table() {
+    ConstD p = (ConstD)kReluPolyTabD;
+    asm volatile("" : "+s"(p));
+    return PolyTab{p};
+}
+// r·u + c with c in an SGPR pair: the VOP3 form (the compiler would copy c to VGPRs
+// for v_fmac_f64 instead)
+__device__ __forceinline__ double fma_sc(double r, double u, double c) {
+    double o;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(u), "s"(c));
+    return o;
+}
+__device__ __forceinline__ double relu_poly(double u, const PolyTab& t) {
+    double r = fma_sc(t.d[kReluPolyDegD], u, t.d[kReluPolyDegD - 1]);
+#pragma unroll
+    for (int k = kReluPolyDegD - 2; k >= 0; --k) r = fma_sc(r, u, t.d[k]);
+    return r;
+}
+__device__ __forceinline__ float relu_poly(float u, const PolyTab&) { return relu_poly(u); }
+
+template <typename T>
+__device__ __forceinline__ T relu_fast(T c, T v1, T v2, const PolyTab& tab) {
+    const T t = v1 * v2 + K<T>::tiny;
+    const T y = rsqrt_fast(t);
+    const T st = t * y;                                     // sqrt(t)
+    const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
+    const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
+    const T xs = fmax_t(x, K<T>::xfloor);
+    const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
+    const T p = relu_poly(fma_t(T(4), x, T(-1)), tab);
+    const T pos = fmax_t(c, T(0));
+    return fma_t((st * x) * sx, p, T(0.5) * pos) + (c - c);
+}
+
 template <typename T>
 __device__ __forceinline__ T relu_fast(T c, T v1, T v2) {
     const T t = v1 * v2 + K<T>::tiny;

@@ -93,7 +93,10 @@ struct NG {
     X(16, 16, 8, 8, 3, 2, -1)          \
     X(16, 16, 8, 8, 1, 2, 0)           \
     X(8, 8, 8, 8, 3, 1, -1)            \
-    X(8, 8, 1, 1, 8, 1, 0)
+    X(8, 8, 1, 1, 8, 1, 0)             \
+    X(14, 14, 1, 1, 14, 1, 0)          \
+    X(16, 16, 1, 1, 16, 1, 0)          \
+    X(32, 32, 1, 1, 32, 1, 0)
 
 struct GeoRow {
     int h, w, ho, wo, taps, s, off, hs_elems;
@@ -161,6 +164,15 @@ __device__ __forceinline__ int opaque_tid() {
     return t;
 }
 
+// global-address-space views: pointers read from the op table are generic, and flat
+// loads would also count in lgkmcnt, so every LDS wait would drain them
+template <typename T>
+using GP = const __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ GP<T> gptr(const void* p) {
+    return (GP<T>)(const T*)p;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -183,25 +195,87 @@ struct NetP {
 // EXACT (CGP_FLAG_EXACT_RELU) is a separate instantiation: a call to the out-of-line
 // relu_exact would make every register live across it caller-saved
 template <bool EXACT, typename T>
-__device__ __forceinline__ T relu_of(T c, T v1, T v2) {
+__device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
     if constexpr (EXACT)
         return relu_exact_inl(c, v1, v2);
     else
-        return relu_fast(c, v1, v2);
+        return relu_fast(c, v1, v2, tab);
+}
+
+// Elementwise-op map sizes with a compile-time instantiation (cgp_net_resolution); any
+// other size runs the generic runtime-size path.
+#define CGP_NET_RESOLUTIONS(X) X(28, 28) X(14, 14) X(7, 7) X(32, 32) X(16, 16) X(8, 8) X(1, 1)
+
+struct ResRow {
+    int h, w;
+};
+#define CGP_NET_RES_ROW(h, w) {h, w},
+constexpr ResRow kResTable[] = {CGP_NET_RESOLUTIONS(CGP_NET_RES_ROW)};
+#undef CGP_NET_RES_ROW
+constexpr int kNumRes = sizeof(kResTable) / sizeof(kResTable[0]);
+constexpr int res_index(int h, int w) {
+    for (int n = 0; n < kNumRes; ++n)
+        if (kResTable[n].h == h && kResTable[n].w == w) return n;
+    return -1;
+}
+
+// Output stage shared by every op: v (R results at LDS offsets at[k] of the dst/add
+// class, variance-map pixels px[k]) -> [ReLU] -> [+ add] -> dst, and optionally
+// relu(result) -> dst2 (the next block's ReLU branch input, saving a separate op).
+// An op has the ReLU or dst2, never both, so one set of prefetched variances (u1, u2)
+// serves either.
+template <typename T, bool EX, bool DU, int R>
+__device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& op, T (&v)[R],
+                                        const int (&at)[R], const bool (&ok)[R],
+                                        const T (&u1)[R], const T (&u2)[R],
+                                        const PolyTab& tab) {
+    if (op.relu) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) v[k] = relu_of<EX>(v[k], u1[k], u2[k], tab);
+    }
+    if (op.add >= 0) {
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            if (ok[k]) v[k] += lds[op.add + at[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+        if (ok[k]) lds[op.dst + at[k]] = v[k];
+    if (DU && op.dst2 >= 0) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) v[k] = relu_of<EX>(v[k], u1[k], u2[k], tab);
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            if (ok[k]) lds[op.dst2 + at[k]] = v[k];
+    }
+}
+
+// variances for the op's ReLU (var_x/var_y) or its dst2 ReLU (var2_x/var2_y)
+template <typename T>
+struct VarSrc {
+    GP<T> x, y;
+    bool on;
+};
+template <typename T>
+__device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, unsigned j,
+                                             int hw) {
+    const bool two = op.dst2 >= 0;
+    VarSrc<T> r;
+    r.on = op.relu != 0 || two;
+    r.x = gptr<T>(two ? op.var2_x : op.var_x) + (size_t)i * hw;
+    r.y = gptr<T>(two ? op.var2_y : op.var_y) + (size_t)j * hw;
+    return r;
 }
 
 // ---- CGP_NET_CONV -------------------------------------------------------------------
-template <typename T, bool EX, class G>
+template <typename T, bool EX, bool DU, class G>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, unsigned i, unsigned j) {
     const int tid = opaque_tid();
+    const PolyTab tab = poly_table();
     const T w = T(op.weight), b = T(op.bias);
-    const bool relu = op.relu != 0, add = op.add >= 0;
-    const T* __restrict__ vx = static_cast<const T*>(op.var_x) + (size_t)i * G::HOWO;
-    const T* __restrict__ vy = static_cast<const T*>(op.var_y) + (size_t)j * G::HOWO;
+    const VarSrc<T> vs = var_src<T>(op, i, j, G::HOWO);
     const T* __restrict__ src = lds + op.src;
-    T* __restrict__ dst = lds + op.dst;
-    const T* __restrict__ ad = lds + (add ? op.add : 0);
     const int wsi = op.ws_in, wso = op.ws_out;
 
     if constexpr (G::REDUCE) {
@@ -220,52 +294,54 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if ((tid & 63) == 0) part[tid >> 6] = acc;
         lds_barrier();
         if (tid == 0) {
-            T v = w * (part[0] + part[1]) + b;
-            if (relu) v = relu_of<EX>(v, vx[0], vy[0]);
-            if (add) v += ad[0];
-            dst[0] = v;
+            T v[1] = {w * (part[0] + part[1]) + b};
+            const int at[1] = {0};
+            const bool ok[1] = {true};
+            T u1[1] = {T(1)}, u2[1] = {T(1)};
+            if (vs.on) {
+                u1[0] = vs.x[0];
+                u2[0] = vs.y[0];
+            }
+            net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::POINT) {
         constexpr int KP = (G::HOWO + kNT - 1) / kNT;
-        T v1[KP], v2[KP];
-        if (relu) {
-#pragma unroll
-            for (int k = 0; k < KP; ++k) {
-                const int px = tid + k * kNT;
-                if (G::HOWO % kNT == 0 || px < G::HOWO) {
-                    v1[k] = vx[px];
-                    v2[k] = vy[px];
-                }
-            }
-        }
+        T u1[KP], u2[KP], v[KP];
+        int at[KP];
+        bool ok[KP];
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             const int px = tid + k * kNT;
-            if (G::HOWO % kNT == 0 || px < G::HOWO) {
-                const int r = px / G::WO, c = px - r * G::WO;
-                T v = w * src[(r * G::S) * wsi + c * G::S] + b;
-                if (relu) v = relu_of<EX>(v, v1[k], v2[k]);
-                if (add) v += ad[r * wso + c];
-                dst[r * wso + c] = v;
-            }
+            ok[k] = G::HOWO % kNT == 0 || px < G::HOWO;
+            const int pc = ok[k] ? px : 0;
+            const int r = pc / G::WO, c = pc - r * G::WO;
+            at[k] = r * wso + c;
+            u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
+            u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
+            v[k] = w * src[(r * G::S) * wsi + c * G::S] + b;
         }
+        net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
     } else {
         T* __restrict__ hs = lds + p.hs;
         // variances of this thread's outputs, in flight during the row pass
-        T v1[G::KV][G::R3], v2[G::KV][G::R3];
-        if (relu) {
+        T u1[G::KV][G::R3], u2[G::KV][G::R3];
+        if (vs.on) {
 #pragma unroll
             for (int kv = 0; kv < G::KV; ++kv) {
                 const int it = tid + kv * kNT;
-                if (G::NV % kNT == 0 || it < G::NV) {
-                    const int g3 = it / G::WO, c = it - g3 * G::WO;
+                const int itc = (G::NV % kNT == 0 || it < G::NV) ? it : 0;
+                const int g3 = itc / G::WO, c = itc - g3 * G::WO;
 #pragma unroll
-                    for (int k = 0; k < G::R3; ++k) {
-                        v1[kv][k] = vx[(g3 * G::R3 + k) * G::WO + c];
-                        v2[kv][k] = vy[(g3 * G::R3 + k) * G::WO + c];
-                    }
+                for (int k = 0; k < G::R3; ++k) {
+                    u1[kv][k] = vs.x[(g3 * G::R3 + k) * G::WO + c];
+                    u2[kv][k] = vs.y[(g3 * G::R3 + k) * G::WO + c];
                 }
             }
+        } else {
+#pragma unroll
+            for (int kv = 0; kv < G::KV; ++kv)
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k) u1[kv][k] = u2[kv][k] = T(1);
         }
         // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
 #pragma unroll
@@ -294,7 +370,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             }
         }
         lds_barrier();
-        // column pass + epilogue
+        // column pass + output stage (uniform branches outside the per-pixel loops: each
+        // stage is one basic block, so the R3 independent ReLUs interleave)
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
@@ -304,66 +381,96 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
-                T o[G::R3];
+                T o[G::R3], v[G::R3];
                 win_sums<T, G::TAPS, G::S, G::R3>(win, o);
+                int at[G::R3];
+                bool ok[G::R3];
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
-                    const int r = g3 * G::R3 + k;
-                    T v = w * o[k] + b;
-                    if (relu) v = relu_of<EX>(v, v1[kv][k], v2[kv][k]);
-                    if (add) v += ad[r * wso + c];
-                    dst[r * wso + c] = v;
+                    v[k] = w * o[k] + b;
+                    at[k] = (g3 * G::R3 + k) * wso + c;
+                    ok[k] = true;
                 }
+                net_out<T, EX, DU, G::R3>(lds, op, v, at, ok, u1[kv], u2[kv], tab);
             }
         }
     }
 }
 
 // ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
-template <typename T, bool EX, int KIND>
+// H_ = W_ = 0: runtime map size (generic path).
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_>
 __device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, unsigned i, unsigned j) {
+    constexpr bool RT = H_ == 0;
+    constexpr int KF = (H_ * W_ + kNT - 1) / kNT;
+    constexpr int KE = RT ? kEw : (KF < kEw ? KF : kEw);   // pixels per thread per pass
     const int tid = opaque_tid();
-    const int wd = op.w, hw = op.h * op.w, ws = op.ws_out;
+    const PolyTab tab = poly_table();
+    const int wd = RT ? op.w : W_, hw = RT ? op.h * op.w : H_ * W_, ws = op.ws_out;
     const FastDiv fw{op.div_m, op.div_s, (unsigned)op.w};
-    const bool add = op.add >= 0;
-    const T* __restrict__ vx = static_cast<const T*>(op.var_x) + (size_t)i * hw;
-    const T* __restrict__ vy = static_cast<const T*>(op.var_y) + (size_t)j * hw;
-    const T* __restrict__ xi = p.x + (size_t)i * p.channels * hw;
-    const T* __restrict__ yj = p.y + (size_t)j * p.channels * hw;
-    for (int base = 0; base < hw; base += kEw * kNT) {
-        T a[kEw], v1[kEw], v2[kEw];
+    // RELU: the op's own ReLU reads (var_x, var_y) = variances of src; dst2 is not allowed
+    const GP<T> vx = gptr<T>(op.var_x) + (size_t)i * hw;
+    const GP<T> vy = gptr<T>(op.var_y) + (size_t)j * hw;
+    const VarSrc<T> vs2 = var_src<T>(op, i, j, hw);   // LINEAR: dst2 variances
+    const GP<T> xi = gptr<T>(p.x) + (size_t)i * p.channels * hw;
+    const GP<T> yj = gptr<T>(p.y) + (size_t)j * p.channels * hw;
+    for (int base = 0; base < hw; base += KE * kNT) {
+        T a[KE], u1[KE], u2[KE];
+        int at[KE];
+        bool ok[KE];
 #pragma unroll
-        for (int k = 0; k < kEw; ++k) {
+        for (int k = 0; k < KE; ++k) {
             const int px = base + k * kNT + tid;
-            if (px < hw) {
-                if constexpr (KIND == CGP_NET_RELU) {
-                    v1[k] = vx[px];
-                    v2[k] = vy[px];
-                } else if constexpr (KIND == CGP_NET_MOMENTS) {
-                    T acc = xi[px] * yj[px];
-                    for (int ch = 1; ch < p.channels; ++ch)
-                        acc += xi[(size_t)ch * hw + px] * yj[(size_t)ch * hw + px];
-                    a[k] = acc / T(p.channels);
-                }
+            ok[k] = (!RT && (H_ * W_) % kNT == 0) || px < hw;
+            const int pc = ok[k] ? px : 0;
+            const int r = RT ? (int)fdiv((unsigned)pc, fw) : pc / W_;
+            at[k] = r * ws + (pc - r * wd);
+            if constexpr (KIND == CGP_NET_RELU) {
+                u1[k] = ok[k] ? vx[pc] : T(1);
+                u2[k] = ok[k] ? vy[pc] : T(1);
+                a[k] = lds[op.src + at[k]];
+            } else if constexpr (KIND == CGP_NET_MOMENTS) {
+                T acc = xi[pc] * yj[pc];
+                for (int ch = 1; ch < p.channels; ++ch)
+                    acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
+                a[k] = acc / T(p.channels);
+                u1[k] = u2[k] = T(1);
+            } else {
+                a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
+                u1[k] = (vs2.on && ok[k]) ? vs2.x[pc] : T(1);
+                u2[k] = (vs2.on && ok[k]) ? vs2.y[pc] : T(1);
             }
         }
+        if constexpr (KIND == CGP_NET_RELU) {
+            // pixels of wholly idle waves are skipped (uniform per wave)
 #pragma unroll
-        for (int k = 0; k < kEw; ++k) {
-            const int px = base + k * kNT + tid;
-            if (px < hw) {
-                const int r = (int)fdiv((unsigned)px, fw), c = px - r * wd;
-                const int at = r * ws + c;
-                T v;
-                if constexpr (KIND == CGP_NET_RELU) {
-                    v = relu_of<EX>(lds[op.src + at], v1[k], v2[k]);
-                    if (add) v += lds[op.add + at];
-                } else if constexpr (KIND == CGP_NET_LINEAR) {
-                    v = T(op.weight) * lds[op.src + at] + T(op.bias) * lds[op.add + at];
-                } else {
-                    v = a[k];
-                }
-                lds[op.dst + at] = v;
+            for (int k = 0; k < KE; ++k)
+                if (base + k * kNT < hw) a[k] = relu_of<EX>(a[k], u1[k], u2[k], tab);
+            if (op.add >= 0) {
+#pragma unroll
+                for (int k = 0; k < KE; ++k)
+                    if (ok[k]) a[k] += lds[op.add + at[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < KE; ++k)
+                if (ok[k]) lds[op.dst + at[k]] = a[k];
+        } else if constexpr (KIND == CGP_NET_MOMENTS) {
+#pragma unroll
+            for (int k = 0; k < KE; ++k)
+                if (ok[k]) lds[op.dst + at[k]] = a[k];
+        } else {
+            // LINEAR: dst = a (no ReLU of its own; add already folded in) [, dst2]
+#pragma unroll
+            for (int k = 0; k < KE; ++k)
+                if (ok[k]) lds[op.dst + at[k]] = a[k];
+            if (DU && op.dst2 >= 0) {
+#pragma unroll
+                for (int k = 0; k < KE; ++k)
+                    if (base + k * kNT < hw) a[k] = relu_of<EX>(a[k], u1[k], u2[k], tab);
+#pragma unroll
+                for (int k = 0; k < KE; ++k)
+                    if (ok[k]) lds[op.dst2 + at[k]] = a[k];
             }
         }
     }
@@ -395,11 +502,33 @@ constexpr int geo_index(int h, int w, int ho, int wo, int k, int s, int o) {
 
 #define CGP_NET_CASE(h, w, ho, wo, k, s, o)                                          \
     case geo_index(h, w, ho, wo, k, s, o):                                           \
-        net_conv<T, EX, NG<h, w, ho, wo, k, s, o>>(lds, op, p, i, j);                    \
+        net_conv<T, EX, DU, NG<h, w, ho, wo, k, s, o>>(lds, op, p, i, j);                    \
         break;
 
-template <typename T, bool EX>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void net_kernel(const NetP<T> p) {
+#define CGP_NET_RES_CASE(h, w)                                                        \
+    case res_index(h, w):                                                             \
+        net_elem<T, EX, DU, KIND, h, w>(lds, op, p, i, j);                                \
+        break;
+
+// only the ReLU is worth a per-size instantiation (MOMENTS runs once per pair, LINEAR
+// only for Mixture / multi-term Sum); fewer cases also keep the SGPR budget
+template <typename T, bool EX, bool DU, int KIND>
+__device__ __forceinline__ void net_elem_dispatch(T* __restrict__ lds, const cgp_net_op& op,
+                                                  const NetP<T>& p, unsigned i, unsigned j) {
+    if constexpr (KIND == CGP_NET_RELU) {
+        switch (op.code) {
+            CGP_NET_RESOLUTIONS(CGP_NET_RES_CASE)
+        default:
+            net_elem<T, EX, DU, KIND, 0, 0>(lds, op, p, i, j);
+            break;
+        }
+    } else {
+        net_elem<T, EX, DU, KIND, 0, 0>(lds, op, p, i, j);
+    }
+}
+
+template <typename T, bool EX, bool DU>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : 4))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
@@ -437,13 +566,13 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
                 }
                 break;
             case CGP_NET_RELU:
-                net_elem<T, EX, CGP_NET_RELU>(lds, op, p, i, j);
+                net_elem_dispatch<T, EX, DU, CGP_NET_RELU>(lds, op, p, i, j);
                 break;
             case CGP_NET_MOMENTS:
-                net_elem<T, EX, CGP_NET_MOMENTS>(lds, op, p, i, j);
+                net_elem_dispatch<T, EX, DU, CGP_NET_MOMENTS>(lds, op, p, i, j);
                 break;
             case CGP_NET_LINEAR:
-                net_elem<T, EX, CGP_NET_LINEAR>(lds, op, p, i, j);
+                net_elem_dispatch<T, EX, DU, CGP_NET_LINEAR>(lds, op, p, i, j);
                 break;
             default:
                 break;
@@ -459,15 +588,43 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
 }
 
-template <typename T, bool EX>
+template <typename T, bool EX, bool DU>
 int net_occupancy(int lds_bytes) {
+    const void* fn = reinterpret_cast<const void*>(net_kernel<T, EX, DU>);
+    if (lds_bytes > 64 * 1024 &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, net_kernel<T, EX>, kNT, lds_bytes) !=
-        hipSuccess) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, net_kernel<T, EX, DU>, kNT,
+                                                     lds_bytes) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
     return n;
+}
+
+template <typename T>
+int net_occupancy_for(int lds_bytes, int flags) {
+    const bool ex = flags & CGP_FLAG_EXACT_RELU, du = flags & CGP_FLAG_NET_DUAL;
+    if (ex) return du ? net_occupancy<T, true, true>(lds_bytes)
+                      : net_occupancy<T, true, false>(lds_bytes);
+    return du ? net_occupancy<T, false, true>(lds_bytes) : net_occupancy<T, false, false>(lds_bytes);
+}
+
+template <typename T, bool EX, bool DU>
+int net_launch(const NetP<T>& p, long long lds_bytes, void* stream) {
+    const int per_cu = net_occupancy<T, EX, DU>((int)lds_bytes);
+    if (per_cu <= 0)
+        return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", lds_bytes);
+    long long grid = (long long)per_cu * device_cus();
+    if (grid > p.units) grid = p.units;
+    grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
+    hipLaunchKernelGGL((net_kernel<T, EX, DU>), dim3((unsigned)grid), dim3(kNT),
+                       (size_t)lds_bytes, as_stream(stream), p);
+    return check_launch("net_kernel");
 }
 
 template <typename T>
@@ -512,25 +669,12 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.hs = a->hs;
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
-    const void* fn = p.exact ? reinterpret_cast<const void*>(net_kernel<T, true>)
-                             : reinterpret_cast<const void*>(net_kernel<T, false>);
-    if (lds_bytes > 64 * 1024)
-        CGP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_bytes));
-    const int per_cu = p.exact ? net_occupancy<T, true>((int)lds_bytes)
-                               : net_occupancy<T, false>((int)lds_bytes);
-    if (per_cu <= 0) return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS",
-                                 lds_bytes);
-    long long grid = (long long)per_cu * device_cus();
-    if (grid > p.units) grid = p.units;
-    grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
+    const bool du = (a->flags & CGP_FLAG_NET_DUAL) != 0;
     if (p.exact)
-        hipLaunchKernelGGL((net_kernel<T, true>), dim3((unsigned)grid), dim3(kNT),
-                           (size_t)lds_bytes, as_stream(stream), p);
-    else
-        hipLaunchKernelGGL((net_kernel<T, false>), dim3((unsigned)grid), dim3(kNT),
-                           (size_t)lds_bytes, as_stream(stream), p);
-    return check_launch("net_kernel");
+        return du ? net_launch<T, true, true>(p, lds_bytes, stream)
+                  : net_launch<T, true, false>(p, lds_bytes, stream);
+    return du ? net_launch<T, false, true>(p, lds_bytes, stream)
+              : net_launch<T, false, false>(p, lds_bytes, stream);
 }
 
 }  // namespace
@@ -548,6 +692,8 @@ int cgp_net_geometry(int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t taps,
     return -1;
 }
 
+int cgp_net_resolution(int32_t h, int32_t w) { return res_index(h, w); }
+
 size_t cgp_net_op_size(void) { return sizeof(cgp_net_op); }
 size_t cgp_net_args_size(void) { return sizeof(cgp_net_args); }
 
@@ -555,18 +701,10 @@ int cgp_net_hs_elems(int32_t code) {
     return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;
 }
 
-int cgp_net_occupancy(int32_t lds_bytes, int32_t f64) {
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags) {
     if (lds_bytes <= 0 || lds_bytes > 160 * 1024) return 0;
-    if (lds_bytes > 64 * 1024) {
-        const void* fn = f64 ? reinterpret_cast<const void*>(net_kernel<double, false>)
-                             : reinterpret_cast<const void*>(net_kernel<float, false>);
-        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
-            hipSuccess) {
-            (void)hipGetLastError();
-            return 0;
-        }
-    }
-    return f64 ? net_occupancy<double, false>(lds_bytes) : net_occupancy<float, false>(lds_bytes);
+    return f64 ? net_occupancy_for<double>(lds_bytes, flags)
+               : net_occupancy_for<float>(lds_bytes, flags);
 }
 
 int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }

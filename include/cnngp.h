@@ -218,15 +218,20 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
 
 typedef struct cgp_net_op {
     int32_t kind;          /* CGP_NET_* */
-    int32_t code;          /* CONV: cgp_net_geometry() of the conv */
+    int32_t code;          /* CONV: cgp_net_geometry();  RELU/LINEAR/MOMENTS:
+                              cgp_net_resolution() of the map, or -1 (generic) */
     int32_t src, dst, add; /* LDS element offsets of the slots' (0, 0) pixel; add < 0: none */
     int32_t ws_in, ws_out; /* row strides (elements) of the src slot / dst and add slots */
     int32_t relu;          /* CONV: apply the ReLU map to the conv output (then + add) */
     int32_t h, w;          /* RELU / LINEAR / MOMENTS: map size (CONV: output size) */
     uint32_t div_m, div_s; /* w as a multiply-high divisor (host: make_fastdiv(w)) */
+    int32_t dst2;          /* CONV/RELU/LINEAR: also write relu(result) here (< 0: no) */
+    int32_t reserved;
     double weight, bias;   /* CONV: w·Σ + b;  LINEAR: dst = weight·src + bias·add */
     const void* var_x;     /* ReLU input variances of the x images, [n1][h·w] */
     const void* var_y;     /* ... of the y images, [n2][h·w] */
+    const void* var2_x;    /* dst2's ReLU: variances of the result, [n1][h·w] */
+    const void* var2_y;    /* [n2][h·w] */
 } cgp_net_op;
 
 typedef struct cgp_net_args {
@@ -253,8 +258,13 @@ int cgp_net_geometry(int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t taps,
 int cgp_net_hs_elems(int32_t code);
 size_t cgp_net_op_size(void);
 size_t cgp_net_args_size(void);
+/* Elementwise-op size code for cgp_net_op.code, or -1 (generic runtime-size path). */
+int cgp_net_resolution(int32_t h, int32_t w);
+/* cgp_net_args.flags: CGP_FLAG_EXACT_RELU, and CGP_FLAG_NET_DUAL when any op has dst2
+ * (selects the kernel instantiation with the dual output stage) */
+#define CGP_FLAG_NET_DUAL 4
 /* workgroups per CU the fused kernel reaches with lds_bytes of LDS (0 if it cannot run) */
-int cgp_net_occupancy(int32_t lds_bytes, int32_t f64);
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags);
 int cgp_net_f64(const cgp_net_args* args, void* stream);
 int cgp_net_f32(const cgp_net_args* args, void* stream);
 

@@ -102,6 +102,9 @@ def run_pair(net, x_i, y_j, var, i, j):
             if f["add"] >= 0:
                 out = out + lds[plane(f["add"], ho, wo, f["ws_out"])]
             lds[plane(f["dst"], ho, wo, f["ws_out"])] = out
+            if f.get("dst2", -1) >= 0:
+                vx, vy = var[f["var2"]]
+                lds[plane(f["dst2"], ho, wo, f["ws_out"])] = _relu(out, vx[i], vy[j])
             lds[hs0:hs0 + 2] = 0.0
         elif kind == 1:                                         # RELU
             h, w = f["h"], f["w"]
@@ -115,6 +118,9 @@ def run_pair(net, x_i, y_j, var, i, j):
             out = f["weight"] * lds[plane(f["src"], h, w, f["ws_in"])] + \
                 f["bias"] * lds[plane(f["add"], h, w, f["ws_out"])]
             lds[plane(f["dst"], h, w, f["ws_out"])] = out
+            if f.get("dst2", -1) >= 0:
+                vx, vy = var[f["var2"]]
+                lds[plane(f["dst2"], h, w, f["ws_out"])] = _relu(out, vx[i], vy[j])
     return lds[net.final_slot]
 
 
