@@ -14,9 +14,10 @@ Fusion uses rules 1-2 of program.fuse (conv→ReLU epilogue, 2-term Sum folded i
 producer); both are exact (IEEE addition commutes).  A ReLU feeding two consumers and the
 input moments stay standalone ops: in LDS they cost no extra memory pass.
 
-Slots.  Every value lives in a slot of its spatial class (H, W): a row-major plane with
-HL zero columns left and HR right of each row (the widest halo any conv reading that
-class needs), row stride ws = HL + W + HR.  Halos are zeroed once per workgroup and never
+Slots.  Every value lives in a slot of its spatial class (H, W): a row-major plane whose
+rows are separated by max(HL, HR) zero columns (HL / HR: the widest left / right halo any
+conv reading that class needs; row r's right halo and row r+1's left halo share the gap),
+row stride ws = W + max(HL, HR), with HL zeros before row 0 and HR after the last row.  Halos are zeroed once per workgroup and never
 written, so convs read padding as zeros.  Rows need no halo: the conv's row-sum scratch
 carries zero rows instead.  Slots are reused as soon as their value is dead, including
 in place (dst == src) — safe because every op reads a pixel before the same thread
@@ -98,10 +99,12 @@ class NetPlan:
                 hl = halo[tuple(op.shape_in)]
                 hl[0] = max(hl[0], lft)
                 hl[1] = max(hl[1], rgt)
-        self.ws = {c: hl[0] + c[1] + hl[1] for c, hl in halo.items()}
+        # rows share their zero gap: row r's right halo and row r+1's left halo are the
+        # same max(HL, HR) columns; the slot adds HL before row 0 and HR after the last
+        self.ws = {c: c[1] + max(hl) for c, hl in halo.items()}
 
         def slot_elems(c):
-            n = c[0] * self.ws[c]
+            n = halo[c][0] + c[0] * self.ws[c] + halo[c][1]
             return (n + ALIGN - 1) // ALIGN * ALIGN
 
         # 3. lower to a linear op list with explicit LINEAR chains

@@ -174,18 +174,62 @@ __device__ __forceinline__ double relu_poly(double u, const PolyTab& t) {
 }
 __device__ __forceinline__ float relu_poly(float u, const PolyTab&) { return relu_poly(u); }
 
+// The same map, trimmed for the whole-network kernel (39 instead of 45 VALU ops):
+// t in one rounding (fma), 0.5·max(c, 0) as 0.25·(c + |c|) — exact, and NaN in c
+// propagates through the add, so the (c - c) term is not needed.
 template <typename T>
 __device__ __forceinline__ T relu_fast(T c, T v1, T v2, const PolyTab& tab) {
-    const T t = v1 * v2 + K<T>::tiny;
+    const T t = fma_t(v1, v2, K<T>::tiny);
     const T y = rsqrt_fast(t);
     const T st = t * y;                                     // sqrt(t)
     const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
     const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
     const T xs = fmax_t(x, K<T>::xfloor);
     const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
-    const T p = relu_poly(fma_t(T(4), x, T(-1)), tab);
-    const T pos = fmax_t(c, T(0));
-    return fma_t((st * x) * sx, p, T(0.5) * pos) + (c - c);
+    const T p = relu_poly(fma_t(T(-2), a, T(1)), tab);      // P(4x - 1)
+    const T hpos = (c + fabs_t(c)) * T(0.25);               // max(c, 0) / 2
+    return fma_t((st * x) * sx, p, hpos);
+}
+
+// R independent ReLUs evaluated stage by stage (stage-major source order).  The SGPR
+// Horner steps are inline asm, which the scheduler keeps in source order, so a per-pixel
+// loop would run R dependent 16-step chains back to back; interleaved here, every step
+// has R independent FMAs in flight.  Same arithmetic as relu_fast(c, v1, v2, tab).
+template <int R>
+__device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R],
+                                            const double (&v2)[R], const PolyTab& tab) {
+    double y[R], st[R], a[R], sx[R], u[R], p[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double t = __builtin_fma(v1[r], v2[r], K<double>::tiny);
+        y[r] = rsqrt_fast(t);
+        st[r] = t * y[r];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        a[r] = __builtin_fmin(__builtin_fabs(c[r] * y[r]), 1.0);
+        const double x = __builtin_fma(-0.5, a[r], 0.5);
+        const double xs = __builtin_fmax(x, K<double>::xfloor);
+        sx[r] = (st[r] * x) * (xs * rsqrt_fast(xs));
+        u[r] = __builtin_fma(-2.0, a[r], 1.0);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) p[r] = fma_sc(tab.d[kReluPolyDegD], u[r], tab.d[kReluPolyDegD - 1]);
+#pragma unroll
+    for (int k = kReluPolyDegD - 2; k >= 0; --k) {
+        const double ck = tab.d[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        c[r] = __builtin_fma(sx[r], p[r], (c[r] + __builtin_fabs(c[r])) * 0.25);
+}
+template <int R>
+__device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],
+                                            const float (&v2)[R], const PolyTab& tab) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = relu_fast(c[r], v1[r], v2[r], tab);
 }
 
 template <typename T>

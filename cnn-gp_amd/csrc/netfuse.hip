@@ -30,6 +30,7 @@ namespace {
 
 constexpr int kNT = 128;        // threads per workgroup: two waves per pair
 constexpr int kST = 8;          // supertile edge: pairs are walked in 8x8 (i, j) blocks
+constexpr int kSTL = 3;         // log2(kST)
 constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
 
 // R | len outputs per item, chosen to minimise rounds·(per-item cost) with ≤ 8 outputs
@@ -201,6 +202,17 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
     else
         return relu_fast(c, v1, v2, tab);
 }
+// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k])
+template <bool EXACT, typename T, int R>
+__device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
+                                       const PolyTab& tab) {
+    if constexpr (EXACT) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) v[k] = relu_exact_inl(v[k], u1[k], u2[k]);
+    } else {
+        relu_fast_n<R>(v, u1, u2, tab);
+    }
+}
 
 // Elementwise-op map sizes with a compile-time instantiation (cgp_net_resolution); any
 // other size runs the generic runtime-size path.
@@ -229,10 +241,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
                                         const int (&at)[R], const bool (&ok)[R],
                                         const T (&u1)[R], const T (&u2)[R],
                                         const PolyTab& tab) {
-    if (op.relu) {
-#pragma unroll
-        for (int k = 0; k < R; ++k) v[k] = relu_of<EX>(v[k], u1[k], u2[k], tab);
-    }
+    if (op.relu) relu_n<EX, T, R>(v, u1, u2, tab);
     if (op.add >= 0) {
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -242,8 +251,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
     for (int k = 0; k < R; ++k)
         if (ok[k]) lds[op.dst + at[k]] = v[k];
     if (DU && op.dst2 >= 0) {
-#pragma unroll
-        for (int k = 0; k < R; ++k) v[k] = relu_of<EX>(v[k], u1[k], u2[k], tab);
+        relu_n<EX, T, R>(v, u1, u2, tab);
 #pragma unroll
         for (int k = 0; k < R; ++k)
             if (ok[k]) lds[op.dst2 + at[k]] = v[k];
@@ -294,7 +302,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if ((tid & 63) == 0) part[tid >> 6] = acc;
         lds_barrier();
         if (tid == 0) {
-            T v[1] = {w * (part[0] + part[1]) + b};
+            T v[1] = {fma_t(w, part[0] + part[1], b)};
             const int at[1] = {0};
             const bool ok[1] = {true};
             T u1[1] = {T(1)}, u2[1] = {T(1)};
@@ -318,7 +326,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             at[k] = r * wso + c;
             u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
             u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
-            v[k] = w * src[(r * G::S) * wsi + c * G::S] + b;
+            v[k] = fma_t(w, src[(r * G::S) * wsi + c * G::S], b);
         }
         net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
     } else {
@@ -387,7 +395,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 bool ok[G::R3];
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
-                    v[k] = w * o[k] + b;
+                    v[k] = fma_t(w, o[k], b);
                     at[k] = (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
@@ -398,85 +406,97 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 }
 
 // ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
-// H_ = W_ = 0: runtime map size (generic path).
-template <typename T, bool EX, bool DU, int KIND, int H_, int W_>
-__device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
-                                         const NetP<T>& p, unsigned i, unsigned j) {
-    constexpr bool RT = H_ == 0;
-    constexpr int KF = (H_ * W_ + kNT - 1) / kNT;
-    constexpr int KE = RT ? kEw : (KF < kEw ? KF : kEw);   // pixels per thread per pass
-    const int tid = opaque_tid();
-    const PolyTab tab = poly_table();
-    const int wd = RT ? op.w : W_, hw = RT ? op.h * op.w : H_ * W_, ws = op.ws_out;
+// One pass: KE pixels per thread at px = base + k·kNT + tid.
+template <typename T, bool EX, bool DU, int KIND, int KE, int W_>
+__device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op& op,
+                                          const NetP<T>& p, unsigned i, unsigned j, int tid,
+                                          int base, int hw, const PolyTab& tab) {
+    const int wd = W_ ? W_ : op.w, ws = op.ws_out;
     const FastDiv fw{op.div_m, op.div_s, (unsigned)op.w};
-    // RELU: the op's own ReLU reads (var_x, var_y) = variances of src; dst2 is not allowed
-    const GP<T> vx = gptr<T>(op.var_x) + (size_t)i * hw;
-    const GP<T> vy = gptr<T>(op.var_y) + (size_t)j * hw;
-    const VarSrc<T> vs2 = var_src<T>(op, i, j, hw);   // LINEAR: dst2 variances
+    // RELU reads (var_x, var_y) = variances of src (an elementwise ReLU has no dst2);
+    // LINEAR may carry a dst2 ReLU with (var2_x, var2_y)
+    const VarSrc<T> vs = KIND == CGP_NET_RELU
+                             ? VarSrc<T>{gptr<T>(op.var_x) + (size_t)i * hw,
+                                         gptr<T>(op.var_y) + (size_t)j * hw, true}
+                             : var_src<T>(op, i, j, hw);
     const GP<T> xi = gptr<T>(p.x) + (size_t)i * p.channels * hw;
     const GP<T> yj = gptr<T>(p.y) + (size_t)j * p.channels * hw;
-    for (int base = 0; base < hw; base += KE * kNT) {
-        T a[KE], u1[KE], u2[KE];
-        int at[KE];
-        bool ok[KE];
+    // waves with no pixel in this pass skip the ReLUs (uniform per wave)
+    const bool live = base + (tid & ~63) < hw;
+    T a[KE], u1[KE], u2[KE];
+    int at[KE];
+    bool ok[KE];
 #pragma unroll
-        for (int k = 0; k < KE; ++k) {
-            const int px = base + k * kNT + tid;
-            ok[k] = (!RT && (H_ * W_) % kNT == 0) || px < hw;
-            const int pc = ok[k] ? px : 0;
-            const int r = RT ? (int)fdiv((unsigned)pc, fw) : pc / W_;
-            at[k] = r * ws + (pc - r * wd);
-            if constexpr (KIND == CGP_NET_RELU) {
-                u1[k] = ok[k] ? vx[pc] : T(1);
-                u2[k] = ok[k] ? vy[pc] : T(1);
-                a[k] = lds[op.src + at[k]];
-            } else if constexpr (KIND == CGP_NET_MOMENTS) {
-                T acc = xi[pc] * yj[pc];
-                for (int ch = 1; ch < p.channels; ++ch)
-                    acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
-                a[k] = acc / T(p.channels);
-                u1[k] = u2[k] = T(1);
-            } else {
-                a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
-                u1[k] = (vs2.on && ok[k]) ? vs2.x[pc] : T(1);
-                u2[k] = (vs2.on && ok[k]) ? vs2.y[pc] : T(1);
-            }
-        }
+    for (int k = 0; k < KE; ++k) {
+        const int px = base + k * kNT + tid;
+        ok[k] = px < hw;
+        const int pc = ok[k] ? px : 0;
+        const int r = W_ ? pc / W_ : (int)fdiv((unsigned)pc, fw);
+        at[k] = r * ws + (pc - r * wd);
+        u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
+        u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
         if constexpr (KIND == CGP_NET_RELU) {
-            // pixels of wholly idle waves are skipped (uniform per wave)
-#pragma unroll
-            for (int k = 0; k < KE; ++k)
-                if (base + k * kNT < hw) a[k] = relu_of<EX>(a[k], u1[k], u2[k], tab);
-            if (op.add >= 0) {
-#pragma unroll
-                for (int k = 0; k < KE; ++k)
-                    if (ok[k]) a[k] += lds[op.add + at[k]];
-            }
-#pragma unroll
-            for (int k = 0; k < KE; ++k)
-                if (ok[k]) lds[op.dst + at[k]] = a[k];
+            a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
-#pragma unroll
-            for (int k = 0; k < KE; ++k)
-                if (ok[k]) lds[op.dst + at[k]] = a[k];
+            T acc = xi[pc] * yj[pc];
+            for (int ch = 1; ch < p.channels; ++ch)
+                acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
+            a[k] = acc / T(p.channels);
         } else {
-            // LINEAR: dst = a (no ReLU of its own; add already folded in) [, dst2]
+            a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
+        }
+    }
+    if constexpr (KIND == CGP_NET_RELU) {
+        if (live) relu_n<EX, T, KE>(a, u1, u2, tab);
+        if (op.add >= 0) {
 #pragma unroll
             for (int k = 0; k < KE; ++k)
-                if (ok[k]) lds[op.dst + at[k]] = a[k];
-            if (DU && op.dst2 >= 0) {
+                if (ok[k]) a[k] += lds[op.add + at[k]];
+        }
+    }
 #pragma unroll
-                for (int k = 0; k < KE; ++k)
-                    if (base + k * kNT < hw) a[k] = relu_of<EX>(a[k], u1[k], u2[k], tab);
+    for (int k = 0; k < KE; ++k)
+        if (ok[k]) lds[op.dst + at[k]] = a[k];
+    if constexpr (KIND == CGP_NET_LINEAR && DU) {
+        if (op.dst2 >= 0) {
+            if (live) relu_n<EX, T, KE>(a, u1, u2, tab);
 #pragma unroll
-                for (int k = 0; k < KE; ++k)
-                    if (ok[k]) lds[op.dst2 + at[k]] = a[k];
-            }
+            for (int k = 0; k < KE; ++k)
+                if (ok[k]) lds[op.dst2 + at[k]] = a[k];
         }
     }
 }
 
-// pair walk: supertile s (8x8 pairs) -> (bi, bj); same tiles enumerate the upper
+// compile-time map size: passes of at most kEw pixels per thread, the last one sized to
+// what is left (28x28: 4 + 3)
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int P>
+__device__ __forceinline__ void elem_passes(T* __restrict__ lds, const cgp_net_op& op,
+                                            const NetP<T>& p, unsigned i, unsigned j,
+                                            int tid, const PolyTab& tab) {
+    constexpr int KF = (H_ * W_ + kNT - 1) / kNT;
+    if constexpr (P * kEw < KF) {
+        constexpr int KE = KF - P * kEw < kEw ? KF - P * kEw : kEw;
+        elem_pass<T, EX, DU, KIND, KE, W_>(lds, op, p, i, j, tid, P * kEw * kNT, H_ * W_, tab);
+        elem_passes<T, EX, DU, KIND, H_, W_, P + 1>(lds, op, p, i, j, tid, tab);
+    }
+}
+
+// H_ = W_ = 0: runtime map size (generic path).
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_>
+__device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
+                                         const NetP<T>& p, unsigned i, unsigned j) {
+    const int tid = opaque_tid();
+    const PolyTab tab = poly_table();
+    if constexpr (H_ == 0) {
+        const int hw = op.h * op.w;
+        for (int base = 0; base < hw; base += kEw * kNT)
+            elem_pass<T, EX, DU, KIND, kEw, 0>(lds, op, p, i, j, tid, base, hw, tab);
+    } else {
+        elem_passes<T, EX, DU, KIND, H_, W_, 0>(lds, op, p, i, j, tid, tab);
+    }
+}
+
+// pair walk: supertile s (kST x kST pairs) -> (bi, bj); same tiles enumerate the upper
 // triangle (bi <= bj) row-major
 __device__ __forceinline__ void tri_decode(unsigned s, unsigned nb, unsigned& bi,
                                            unsigned& bj) {
@@ -528,7 +548,7 @@ __device__ __forceinline__ void net_elem_dispatch(T* __restrict__ lds, const cgp
 }
 
 template <typename T, bool EX, bool DU>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : 4))) void net_kernel(const NetP<T> p) {
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : (DU ? 4 : 5)))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
@@ -541,7 +561,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : 4)
     const long long beg = (long long)xcd * per;
     const long long end = beg + per < p.units ? beg + per : p.units;
     for (long long u = beg + l; u < end; u += g8) {
-        const unsigned s = (unsigned)(u >> 6), q = (unsigned)u & 63u;
+        const unsigned s = (unsigned)(u >> (2 * kSTL)), q = (unsigned)u & (kST * kST - 1u);
         unsigned bi, bj;
         if (p.same) {
             tri_decode(s, p.nbi, bi, bj);
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : 4)
             bi = s / p.nbj;
             bj = s - bi * p.nbj;
         }
-        const unsigned i = bi * kST + (q >> 3), j = bj * kST + (q & 7u);
+        const unsigned i = bi * kST + (q >> kSTL), j = bj * kST + (q & (kST - 1u));
         if (i >= p.n1 || j >= p.n2) continue;
         if (p.same && j <= i) {
             if (j == i && tid == 0) p.out[(long long)i * p.ldo + i] = p.kdiag[i];
@@ -659,8 +679,8 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.nbj = (unsigned)((a->n2 + kST - 1) / kST);
     const long long tiles = a->same ? (long long)p.nbi * (p.nbi + 1) / 2
                                     : (long long)p.nbi * p.nbj;
-    if (tiles * 64 >= (1LL << 40)) return fail(CGP_EINVAL, "net: tile too large");
-    p.units = tiles * 64;
+    if (tiles * kST * kST >= (1LL << 40)) return fail(CGP_EINVAL, "net: tile too large");
+    p.units = tiles * kST * kST;
     p.nops = a->nops;
     p.channels = a->channels;
     p.hw_in = a->h * a->w;
