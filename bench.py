@@ -14,8 +14,9 @@ collective; per-rank work is ~constant ("scaling": "weak").
 
 value = evaluated pairs (Σ over all tiles of B1·B2) per second, whole job.  Also
 reported: unique Kxx entries/s, the single-GPU build+solve wall-clock (rocSOLVER
-dpotrf+dpotrs on the assembled Kxx, NaN lower triangle), the dominant kernel's HBM
-roofline fraction measured live with HIP events, and the CPU oracle's rate on a bounded
+dpotrf+dpotrs on the assembled Kxx, NaN lower triangle), the dominant kernel's
+roofline fraction measured live with HIP events (the whole-network kernel: fp64 compute
+roof; the layer path: HBM roof), and the CPU oracle's rate on a bounded
 sample of the same workload (cpu_baseline).
 """
 from __future__ import annotations
@@ -39,6 +40,8 @@ from cnn_gp import _native as N  # noqa: E402
 from cnn_gp.data import tile_schedule  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
+FP64_PEAK_TFLOPS = 78.6        # MI355X spec FP64 (vector = matrix); half the FP32 157.3
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "net_traffic.json")
 
 
 def parse():
@@ -135,6 +138,68 @@ def probe_kernels(model, x, n1, n2, reps=10):
     plan.run_pairs(x, x, xy0, var, n1, n2, False, False, s, probe=probe)
     torch.cuda.synchronize()
     return res
+
+
+def alg_flops_per_pair(plan):
+    """The reference's direct-stencil conv flops per pair: F.conv2d does
+    2·extent² flops per output pixel (extent = k, or k + 1 for an even "same" kernel).
+    The ReLU arc-cosine arithmetic — the fused kernel's main VALU cost — is not counted."""
+    f = 0
+    for op in plan.prog.ops:
+        if op.kind == "conv":
+            e = op.geom.extent or op.geom.taps
+            f += 2 * e * e * op.shape_out[0] * op.shape_out[1]
+    return f
+
+
+def probe_net(model, x, y, cfg_name, reps=5):
+    """Average duration of the whole-network kernel on one full Kxz tile (x × y), HIP
+    events on the launch stream; plus the per-image variance pipeline it needs."""
+    from cnn_gp.program import Plan
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    n1, C, h, w = x.shape
+    n2 = y.shape[0]
+    plan = model._plan(h, w)
+    net = model._net_plan(plan, x.element_size())
+    if net is None:
+        return None
+    sfx = Plan._sfx(x.dtype)
+    lib = N.load()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
+    N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, C, h * w,
+                                                    N.ptr(var0[:n1]), N.ptr(var0[n1:]), s), "mv")
+    var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, False, s, need=net.need_var)
+    ev[1].record(stream)
+    launch, out = net.prepare(x, y, var, n1, n2, False, plan.flags)
+    launch(s)                                   # warm
+    ev[2].record(stream)
+    for _ in range(reps):
+        launch(s)
+    ev[3].record(stream)
+    ev[3].synchronize()
+    ms = ev[2].elapsed_time(ev[3]) / reps
+    fl = alg_flops_per_pair(plan)
+    kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
+    traffic = None
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f).get(cfg_name)
+        if t and t.get("tile") == n1 and t.get("dtype") == str(x.dtype):
+            traffic = t["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    achieved = fl * n1 * n2 / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic,
+            "kernel": kname, "avg_ms": round(ms, 4), "pairs_per_launch": n1 * n2,
+            "alg_flops_per_pair": fl, "alg_flops_per_launch": fl * n1 * n2,
+            "var_pipeline_ms": round(ev[0].elapsed_time(ev[1]), 4),
+            "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
+            "note": "fp64 compute roof (VALU = MFMA = 78.6 TF on MI355X); algorithmic "
+                    "flops = the reference's direct-stencil conv flops only"}
 
 
 def cpu_baseline(cfg_name, dtype, pairs):
@@ -238,23 +303,27 @@ def main():
     roof = None
     if rank == 0 and not args.no_probe:
         with torch.no_grad():
-            ops = probe_kernels(model, X[:B], B, B)
-        by = {}
-        for name, ms, b in ops:
-            t = by.setdefault(name, [0.0, 0, 0.0, 0])
-            t[0] += ms
-            t[1] += 1
-            t[2] += b
-            t[3] = b
-        dom = max(by.items(), key=lambda kv: kv[1][0])
-        name, (tot_ms, cnt, _, b_launch) = dom
-        avg_ms = tot_ms / cnt
-        achieved = b_launch / (avg_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
-                "alg_bytes_per_launch": int(b_launch)}
-        extra["kernel_breakdown_ms_per_tile"] = {k: round(v[0], 3) for k, v in by.items()}
+            roof = probe_net(model, X[:B], X[B:2 * B] if n_total >= 2 * B else X[:B],
+                             args.config)
+        if roof is None:                         # layer-by-layer path: per-op HBM roofline
+            with torch.no_grad():
+                ops = probe_kernels(model, X[:B], B, B)
+            by = {}
+            for name, ms, b in ops:
+                t = by.setdefault(name, [0.0, 0, 0.0, 0])
+                t[0] += ms
+                t[1] += 1
+                t[2] += b
+                t[3] = b
+            dom = max(by.items(), key=lambda kv: kv[1][0])
+            name, (tot_ms, cnt, _, b_launch) = dom
+            avg_ms = tot_ms / cnt
+            achieved = b_launch / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
+                    "alg_bytes_per_launch": int(b_launch)}
+            extra["kernel_breakdown_ms_per_tile"] = {k: round(v[0], 3) for k, v in by.items()}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

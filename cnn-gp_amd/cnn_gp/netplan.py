@@ -255,16 +255,19 @@ class NetPlan:
                 o.var2_x, o.var2_y = vx.data_ptr(), vy.data_ptr()
         return arr
 
-    def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
-            out: Optional[torch.Tensor] = None):
-        """K tile [n1, n2] of the pairs (x_i, y_j).  var: value -> (xx [n1,..], yy [n2,..])
-        for every value in ``need_var``."""
+    def prepare(self, x, y, var, n1: int, n2: int, same: bool, flags: int = 0,
+                out: Optional[torch.Tensor] = None):
+        """Upload the op list for these variance maps; return (launch(stream), out).
+        ``out`` may be a row-strided view (e.g. a tile of a larger K): the kernel writes
+        K[i, j] at out[i * out.stride(0) + j]."""
         sfx = "f64" if x.dtype == torch.float64 else "f32"
         arr = self._ops_array(var)
         host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         ops_dev = host.to(x.device)                 # stream-ordered, freed stream-ordered
         if out is None:
             out = torch.empty((n1, n2), dtype=x.dtype, device=x.device)
+        if out.shape != (n1, n2) or out.stride(1) != 1 or out.dtype != x.dtype:
+            raise ValueError("out must be an [n1, n2] row-major view of the input dtype")
         a = N.NetArgs()
         a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
         if same:
@@ -276,5 +279,17 @@ class NetPlan:
         a.same, a.final_slot, a.hs, a.lds_elems = int(same), self.final_slot, self.hs, \
             self.lds_elems
         a.flags = flags | (N.CGP_FLAG_NET_DUAL if self.dual else 0)
-        N.check(getattr(N.load(), f"cgp_net_{sfx}")(ctypes.byref(a), stream), "cgp_net")
+        fn = getattr(N.load(), f"cgp_net_{sfx}")
+
+        def launch(stream, a=a, ops_dev=ops_dev, fn=fn):
+            N.check(fn(ctypes.byref(a), stream), "cgp_net")
+
+        return launch, out
+
+    def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
+            out: Optional[torch.Tensor] = None):
+        """K tile [n1, n2] of the pairs (x_i, y_j).  var: value -> (xx [n1,..], yy [n2,..])
+        for every value in ``need_var``."""
+        launch, out = self.prepare(x, y, var, n1, n2, same, flags, out)
+        launch(stream)
         return out

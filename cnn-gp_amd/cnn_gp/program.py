@@ -43,6 +43,7 @@ class ConvGeom:
     dilation: int
     weight: float       # the kernel buffer's value (fp32-rounded unless built in fp64)
     bias: float
+    extent: int = 0     # the reference kernel's edge (k + 1 for an even "same" kernel)
 
 
 @dataclasses.dataclass
@@ -84,6 +85,7 @@ def conv_geometry(mod) -> ConvGeom:
     offset = -pad + (d if mod.kernel_has_row_of_zeros else 0)
     w = float(mod.kernel.reshape(-1)[-1].item())
     return ConvGeom(taps=k, offset=offset, stride=s, dilation=d, weight=w,
+                    extent=k + 1 if mod.kernel_has_row_of_zeros else k,
                     bias=float(mod.var_bias))
 
 

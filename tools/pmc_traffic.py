@@ -1,0 +1,45 @@
+"""HBM traffic per launch of the whole-network kernel from rocprofv3 FETCH_SIZE /
+WRITE_SIZE passes (separate runs of tools/netbench.py on one config), corrected as
+MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) counts half the bytes of wide reads on
+gfx950, so bytes = 2·FETCH_SIZE·1024 + WRITE_SIZE·1024.
+
+    python tools/pmc_traffic.py CONFIG TILE DTYPE FETCH_DIR WRITE_DIR [OUT_JSON]
+"""
+import csv
+import glob
+import json
+import sys
+
+
+def per_launch(d, counter):
+    vals = []
+    for f in glob.glob(d + "/*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if "net_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no net_kernel {counter} rows under {d}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    cfg, tile, dtype, fdir, wdir = sys.argv[1:6]
+    out = sys.argv[6] if len(sys.argv) > 6 else None
+    fetch, nf = per_launch(fdir, "FETCH_SIZE")
+    write, nw = per_launch(wdir, "WRITE_SIZE")
+    rec = {"tile": int(tile), "dtype": dtype, "fetch_size_kb": fetch, "write_size_kb": write,
+           "hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
+           "launches_averaged": [nf, nw],
+           "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)"}
+    print(json.dumps({cfg: rec}, indent=1))
+    if out:
+        try:
+            data = json.load(open(out))
+        except (OSError, ValueError):
+            data = {}
+        data[cfg] = rec
+        json.dump(data, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
