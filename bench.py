@@ -56,8 +56,8 @@ def parse():
     p.add_argument("--no-solve", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-probe", action="store_true")
-    p.add_argument("--cpu-pairs", type=int, default=4096,
-                   help="pairs in the CPU-oracle sample (64x64 tile = 4096)")
+    p.add_argument("--cpu-pairs", type=int, default=16384,
+                   help="pairs in the CPU-oracle sample (128x128 tile = 16384, ~10-30 s)")
     return p.parse_args()
 
 
@@ -152,54 +152,38 @@ def alg_flops_per_pair(plan):
     return f
 
 
-def probe_net(model, x, y, cfg_name, reps=5):
-    """Average duration of the whole-network kernel on one full Kxz tile (x × y), HIP
-    events on the launch stream; plus the per-image variance pipeline it needs."""
-    from cnn_gp.program import Plan
-    stream = torch.cuda.current_stream()
-    s = stream.cuda_stream
-    n1, C, h, w = x.shape
-    n2 = y.shape[0]
+def net_roofline(model, x, cfg_name, timing):
+    """Roofline of the whole-network kernel from the HIP events recorded around each of its
+    launches in the timed region (cnn_gp.netplan.TIMING, on the launch stream)."""
+    n, C, h, w = x.shape
     plan = model._plan(h, w)
     net = model._net_plan(plan, x.element_size())
-    if net is None:
+    if net is None or not timing:
         return None
-    sfx = Plan._sfx(x.dtype)
-    lib = N.load()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    ev[0].record(stream)
-    var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
-    N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, C, h * w,
-                                                    N.ptr(var0[:n1]), N.ptr(var0[n1:]), s), "mv")
-    var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, False, s, need=net.need_var)
-    ev[1].record(stream)
-    launch, out = net.prepare(x, y, var, n1, n2, False, plan.flags)
-    launch(s)                                   # warm
-    ev[2].record(stream)
-    for _ in range(reps):
-        launch(s)
-    ev[3].record(stream)
-    ev[3].synchronize()
-    ms = ev[2].elapsed_time(ev[3]) / reps
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in timing)
+    pairs = sum(p for _, _, p in timing)
     fl = alg_flops_per_pair(plan)
-    kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
+    achieved = fl * pairs / (ms * 1e-3) / 1e12
     traffic = None
     try:
         with open(TRAFFIC_FILE) as f:
             t = json.load(f).get(cfg_name)
-        if t and t.get("tile") == n1 and t.get("dtype") == str(x.dtype):
-            traffic = t["hbm_bytes_per_launch"]
+        if t and t.get("dtype") == str(x.dtype):
+            # measured on one full tile: scale to this run's average launch
+            traffic = int(t["hbm_bytes_per_launch"] / t["tile"] ** 2 * pairs / len(timing))
     except (OSError, ValueError):
         pass
-    achieved = fl * n1 * n2 / (ms * 1e-3) / 1e12
+    kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic,
-            "kernel": kname, "avg_ms": round(ms, 4), "pairs_per_launch": n1 * n2,
-            "alg_flops_per_pair": fl, "alg_flops_per_launch": fl * n1 * n2,
-            "var_pipeline_ms": round(ev[0].elapsed_time(ev[1]), 4),
+            "kernel": kname, "launches": len(timing), "avg_ms": round(ms / len(timing), 4),
+            "pairs_per_launch": pairs // len(timing), "alg_flops_per_pair": fl,
+            "alg_flops_per_launch": fl * pairs // len(timing),
             "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
             "note": "fp64 compute roof (VALU = MFMA = 78.6 TF on MI355X); algorithmic "
-                    "flops = the reference's direct-stencil conv flops only"}
+                    "flops = the reference's direct-stencil conv flops of the pairs the "
+                    "kernel evaluates (same tiles: i < j); traffic: PMC FETCH/WRITE per "
+                    "launch (profiles/r1/net_traffic.json), scaled to this launch size"}
 
 
 def cpu_baseline(cfg_name, dtype, pairs):
@@ -268,6 +252,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    from cnn_gp import netplan
+    netplan.TIMING = [] if rank == 0 and not args.no_probe else None
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -278,6 +264,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    timing, netplan.TIMING = netplan.TIMING, None
     ms_step = elapsed / args.steps * 1e3
     value = pairs_total * args.steps / elapsed
 
@@ -302,9 +289,7 @@ def main():
     # --- dominant kernel, timed live ---
     roof = None
     if rank == 0 and not args.no_probe:
-        with torch.no_grad():
-            roof = probe_net(model, X[:B], X[B:2 * B] if n_total >= 2 * B else X[:B],
-                             args.config)
+        roof = net_roofline(model, X[:B], args.config, timing)
         if roof is None:                         # layer-by-layer path: per-op HBM roofline
             with torch.no_grad():
                 ops = probe_kernels(model, X[:B], B, B)

@@ -35,6 +35,10 @@ from . import _native as N
 from .program import fuse
 
 ALIGN = 2                      # slot bases on 16-byte boundaries (fp64 elements)
+
+# Optional launch timing (bench.py): when a list, every launch appends
+# (start event, end event, pairs evaluated) recorded on the launch stream.
+TIMING = None
 MAX_LDS_BYTES = 160 * 1024
 
 
@@ -281,8 +285,19 @@ class NetPlan:
         a.flags = flags | (N.CGP_FLAG_NET_DUAL if self.dual else 0)
         fn = getattr(N.load(), f"cgp_net_{sfx}")
 
+        pairs = n1 * (n1 - 1) // 2 if same else n1 * n2
+
         def launch(stream, a=a, ops_dev=ops_dev, fn=fn):
-            N.check(fn(ctypes.byref(a), stream), "cgp_net")
+            if TIMING is not None:
+                st = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                N.check(fn(ctypes.byref(a), stream), "cgp_net")
+                e1.record(st)
+                TIMING.append((e0, e1, pairs))
+            else:
+                N.check(fn(ctypes.byref(a), stream), "cgp_net")
 
         return launch, out
 
