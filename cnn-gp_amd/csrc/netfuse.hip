@@ -29,8 +29,11 @@ using namespace cgp;
 namespace {
 
 constexpr int kNT = 128;        // threads per workgroup: two waves per pair
-constexpr int kST = 8;          // supertile edge: pairs are walked in 8x8 (i, j) blocks
-constexpr int kSTL = 3;         // log2(kST)
+#ifndef CGP_NET_STL
+#define CGP_NET_STL 3
+#endif
+constexpr int kSTL = CGP_NET_STL;   // log2(kST)
+constexpr int kST = 1 << kSTL;      // supertile edge: pairs are walked in 8x8 (i, j) blocks
 constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
 
 // R | len outputs per item, chosen to minimise rounds·(per-item cost) with ≤ 8 outputs
@@ -547,8 +550,12 @@ __device__ __forceinline__ void net_elem_dispatch(T* __restrict__ lds, const cgp
     }
 }
 
-template <typename T, bool EX, bool DU>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : (DU ? 4 : 5)))) void net_kernel(const NetP<T> p) {
+// WPE: waves per SIMD the register allocation targets (amdgpu_waves_per_eu).  LDS caps
+// the resident workgroups per CU (two waves each) at 160 KB / footprint, so allocating
+// registers for more waves than that only forces spills; net_launch picks WPE from the
+// LDS footprint (net_wpe).
+template <typename T, bool EX, bool DU, int WPE>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
@@ -608,9 +615,35 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(EX ? 3 : (D
     }
 }
 
-template <typename T, bool EX, bool DU>
-int net_occupancy(int lds_bytes) {
-    const void* fn = reinterpret_cast<const void*>(net_kernel<T, EX, DU>);
+// waves per SIMD the LDS footprint allows (2 waves per workgroup, 4 SIMDs per CU),
+// clamped to the instantiated register targets 3..5
+inline int net_wpe(long long lds_bytes) {
+    const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
+    const long long w = wg / 2;
+    return w < 3 ? 3 : (w > 5 ? 5 : (int)w);
+}
+
+// the instantiation for (EX, DU, LDS footprint): fp64 closed form — the production path
+// — has a register target per occupancy level; the exact ReLU and fp32 one each
+template <typename T>
+const void* net_fn(bool ex, bool du, long long lds_bytes) {
+    if (ex) return du ? (const void*)net_kernel<T, true, true, 3>
+                      : (const void*)net_kernel<T, true, false, 3>;
+    if constexpr (sizeof(T) == 8) {
+        switch (net_wpe(lds_bytes)) {
+        case 3: return du ? (const void*)net_kernel<T, false, true, 3>
+                          : (const void*)net_kernel<T, false, false, 3>;
+        case 4: return du ? (const void*)net_kernel<T, false, true, 4>
+                          : (const void*)net_kernel<T, false, false, 4>;
+        default: return du ? (const void*)net_kernel<T, false, true, 5>
+                           : (const void*)net_kernel<T, false, false, 5>;
+        }
+    }
+    return du ? (const void*)net_kernel<T, false, true, 4>
+              : (const void*)net_kernel<T, false, false, 5>;
+}
+
+int net_occupancy(const void* fn, int lds_bytes) {
     if (lds_bytes > 64 * 1024 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
             hipSuccess) {
@@ -618,8 +651,7 @@ int net_occupancy(int lds_bytes) {
         return 0;
     }
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, net_kernel<T, EX, DU>, kNT,
-                                                     lds_bytes) != hipSuccess) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kNT, lds_bytes) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
@@ -628,22 +660,24 @@ int net_occupancy(int lds_bytes) {
 
 template <typename T>
 int net_occupancy_for(int lds_bytes, int flags) {
-    const bool ex = flags & CGP_FLAG_EXACT_RELU, du = flags & CGP_FLAG_NET_DUAL;
-    if (ex) return du ? net_occupancy<T, true, true>(lds_bytes)
-                      : net_occupancy<T, true, false>(lds_bytes);
-    return du ? net_occupancy<T, false, true>(lds_bytes) : net_occupancy<T, false, false>(lds_bytes);
+    return net_occupancy(net_fn<T>(flags & CGP_FLAG_EXACT_RELU, flags & CGP_FLAG_NET_DUAL,
+                                   lds_bytes),
+                         lds_bytes);
 }
 
-template <typename T, bool EX, bool DU>
-int net_launch(const NetP<T>& p, long long lds_bytes, void* stream) {
-    const int per_cu = net_occupancy<T, EX, DU>((int)lds_bytes);
+template <typename T>
+int net_launch(const NetP<T>& p, bool ex, bool du, long long lds_bytes, void* stream) {
+    const void* fn = net_fn<T>(ex, du, lds_bytes);
+    const int per_cu = net_occupancy(fn, (int)lds_bytes);
     if (per_cu <= 0)
         return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", lds_bytes);
     long long grid = (long long)per_cu * device_cus();
     if (grid > p.units) grid = p.units;
     grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
-    hipLaunchKernelGGL((net_kernel<T, EX, DU>), dim3((unsigned)grid), dim3(kNT),
-                       (size_t)lds_bytes, as_stream(stream), p);
+    NetP<T> arg = p;
+    void* args[] = {&arg};
+    CGP_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args, (size_t)lds_bytes,
+                            as_stream(stream)));
     return check_launch("net_kernel");
 }
 
@@ -690,11 +724,7 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
     const bool du = (a->flags & CGP_FLAG_NET_DUAL) != 0;
-    if (p.exact)
-        return du ? net_launch<T, true, true>(p, lds_bytes, stream)
-                  : net_launch<T, true, false>(p, lds_bytes, stream);
-    return du ? net_launch<T, false, true>(p, lds_bytes, stream)
-              : net_launch<T, false, false>(p, lds_bytes, stream);
+    return net_launch<T>(p, p.exact != 0, du, lds_bytes, stream);
 }
 
 }  // namespace

@@ -419,6 +419,29 @@ def test_edge_shapes_and_zero_images():
     assert np.isfinite(got).all() and (got[1, [0, 2]] > 0).all()
 
 
+@pytest.mark.parametrize("cfg", ["mnist_as_tf", "mnist_paper_convnet_gp"])
+def test_netfuse_zero_variance_pixels_match_oracle(cfg):
+    """MNIST-like images (zero borders, ~60% zero pixels, an all-zero image) through the
+    whole-network kernel: zero-variance pixels (bias-free convs) take ReLU.propagate's
+    f32_tiny path (kernels.py:146) exactly like the reference"""
+    spec = getattr(specs, cfg)()
+    m = configs_util.model(cfg).double().to(DEV)
+    rng = np.random.default_rng(21)
+    X = np.floor(rng.random((6, 1, 28, 28)) * 256) / 255.0
+    X[rng.random(X.shape) < 0.6] = 0.0
+    X[:, :, :4, :] = 0.0
+    X[:, :, -4:, :] = 0.0
+    X[:, :, :, :4] = 0.0
+    X[:, :, :, -4:] = 0.0
+    X[3] = 0.0
+    Z = X[::-1].copy()
+    got = m(dev(X), dev(Z), False, False).cpu().numpy()
+    ref = O.kernel(spec, X, Z, False, False)
+    np.testing.assert_allclose(got, ref, rtol=RTOL64["fast"], atol=1e-300)
+    gxx = m(dev(X)).cpu().numpy()
+    np.testing.assert_allclose(gxx, O.kernel(spec, X), rtol=RTOL64["fast"], atol=1e-300)
+
+
 def test_tiles_assemble_to_full_matrix_and_symmetry():
     """tile vs full: same=False tiles of Kxx equal the full same=True evaluation except
     on the diagonal (override), and Kxx is symmetric + positive definite"""
