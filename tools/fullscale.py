@@ -1,0 +1,166 @@
+"""Full-scale ResNet-GP run (BASELINE.json configs[3]): Kxx of N training images, Kxz of
+M test images against them, then the GP solve and prediction — the whole of
+exp_mnist_resnet/run.bash (save_kernel.py → merge_h5_files.py → classify_gp.py) on the
+device, in memory.
+
+    python tools/fullscale.py [--n 60000 --m 10000 --tile 4096 --config mnist_as_tf]
+    torchrun --nproc-per-node 8 tools/fullscale.py ...   # tiles split, one gather to rank 0
+
+Data: synthetic MNIST-like images (values k/255, ~60% zero pixels, 4-pixel zero border;
+no dataset files here) with synthetic labels, so the accuracy line only proves the path
+runs.  Kxx keeps the reference's layout (upper tiles, NaN strictly-lower tiles) and is
+factored in place by rocSOLVER dpotrf_64 (upper triangle, like scipy's posv).
+
+Checks printed at the end: potrf info (positive definite), a spot check of random Kxx
+and Kxz entries recomputed one pair at a time through model(x_i, x_j, False, False), and
+the solve residual ‖Kxx·α − Y‖ / ‖Y‖ on a random subset of rows.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import cnn_gp  # noqa: E402
+from cnn_gp.data import tile_schedule  # noqa: E402
+from cnn_gp.gram import gather_gram  # noqa: E402
+
+
+def mnist_like(n, C, side, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.floor(torch.rand((n, C, side, side), generator=g, dtype=torch.float64) * 256) / 255
+    x[torch.rand(x.shape, generator=g) < 0.6] = 0.0
+    x[..., :4, :] = 0.0
+    x[..., -4:, :] = 0.0
+    x[..., :, :4] = 0.0
+    x[..., :, -4:] = 0.0
+    return x
+
+
+def log(rank, msg):
+    if rank == 0:
+        print(msg, flush=True)
+
+
+def build(model, X, X2, B, rank, world, out, name, t_start):
+    """This rank's tiles of Kxx (X2 None) or Kxz, written into ``out`` on the device."""
+    n = len(X)
+    tiles = tile_schedule(n, None if X2 is None else len(X2), B, rank, world)
+    pairs = 0
+    last = time.perf_counter()
+    with torch.no_grad():
+        for k, (same, bi, bj) in enumerate(tiles):
+            i0, j0 = bi * B, bj * B
+            x = X[i0:i0 + B]
+            if same:
+                t = model(x)
+            else:
+                src = X if X2 is None else X2
+                t = model(x, src[j0:j0 + B], False, False)
+            out[i0:i0 + t.shape[0], j0:j0 + t.shape[1]].copy_(t)
+            pairs += t.numel() if not same else t.shape[0] * (t.shape[0] + 1) // 2
+            now = time.perf_counter()
+            if now - last > 20:
+                torch.cuda.synchronize()
+                log(rank, f"  {name}: tile {k + 1}/{len(tiles)} "
+                          f"({time.perf_counter() - t_start:.0f} s)")
+                last = now
+    return pairs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="mnist_as_tf")
+    ap.add_argument("--n", type=int, default=60000)
+    ap.add_argument("--m", type=int, default=10000)
+    ap.add_argument("--tile", type=int, default=4096)
+    ap.add_argument("--jitter", type=float, default=0.0)
+    ap.add_argument("--spot", type=int, default=16)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = importlib.import_module(f"configs.{args.config}")
+    model = cfg.initial_model.to(dev, torch.float64)
+    C = getattr(cfg, "in_channels", 1)
+    side = 32 if C == 3 else 28
+    X = mnist_like(args.n, C, side, 0).to(dev)
+    Z = mnist_like(args.m, C, side, 1).to(dev)
+    g = torch.Generator().manual_seed(2)
+    ytr = torch.randint(0, 10, (args.n,), generator=g)
+    yte = torch.randint(0, 10, (args.m,), generator=g)
+    B = args.tile
+    res = {"config": args.config, "n": args.n, "m": args.m, "tile": B, "gpus": world}
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    K = torch.full((args.n, args.n), float("nan"), dtype=torch.float64, device=dev)
+    p_xx = build(model, X, None, B, rank, world, K, "Kxx", t0)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    Kxz = torch.full((args.m, args.n), float("nan"), dtype=torch.float64, device=dev)
+    p_xz = build(model, Z, X, B, rank, world, Kxz, "Kxz", t0)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if world > 1:
+        K = gather_gram(K, args.n, None, B)
+        Kxz = gather_gram(Kxz, args.m, args.n, B)
+        torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    res.update(kxx_s=round(t1 - t0, 2), kxz_s=round(t2 - t1, 2), gather_s=round(t3 - t2, 3),
+               kxx_pairs_per_s_rank0=round(p_xx / (t1 - t0), 1),
+               kxz_pairs_per_s_rank0=round(p_xz / (t2 - t1), 1))
+    log(rank, f"kernels built in {t3 - t0:.1f} s")
+    if rank == 0:
+        # spot check: single pairs through the same drop-in call, other tile shapes
+        gs = torch.Generator().manual_seed(3)
+        ii = torch.randint(0, args.n, (args.spot,), generator=gs)
+        jj = torch.randint(0, args.n, (args.spot,), generator=gs)
+        kk = torch.randint(0, args.m, (args.spot,), generator=gs)
+        worst = 0.0
+        with torch.no_grad():
+            for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
+                a, b = min(a, b), max(a, b)
+                ref = model(X[a:a + 1], X[b:b + 1], a == b, False).item() if a != b else \
+                    model(X[a:a + 1]).item()
+                worst = max(worst, abs(K[a, b].item() - ref) / abs(ref))
+                ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
+                worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
+        res["spot_check_max_rel_err"] = worst
+        # residual rows: K is symmetric, its upper triangle is filled
+        rows = torch.randint(0, args.n, (8,), generator=gs).to(dev)
+        Krows = torch.where(torch.arange(args.n, device=dev)[None, :] >= rows[:, None],
+                            K[rows], K[:, rows].T)
+        Y = cnn_gp.one_hot_pm1(ytr, 10).to(dev)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        A = cnn_gp.solve_system(K, Y, jitter=args.jitter)     # K overwritten by its factor
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        diag_j = torch.arange(len(rows), device=dev)
+        Krows[diag_j, rows] += args.jitter
+        r = (Krows @ A - Y[rows]).norm() / Y[rows].norm()
+        pred = cnn_gp.predict(A, Kxz)
+        t6 = time.perf_counter()
+        acc = cnn_gp.accuracy(pred, yte)
+        res.update(solve_s=round(t5 - t4, 2), solve_tflops=round(args.n ** 3 / 3 / (t5 - t4) / 1e12, 2),
+                   predict_s=round(t6 - t5, 3), residual=float(r),
+                   synthetic_accuracy=acc, total_s=round(t6 - t0, 2))
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
