@@ -290,25 +290,32 @@ def main():
     roof = None
     if rank == 0 and not args.no_probe:
         roof = net_roofline(model, X[:B], args.config, timing)
-        if roof is None:                         # layer-by-layer path: per-op HBM roofline
-            with torch.no_grad():
-                ops = probe_kernels(model, X[:B], B, B)
-            by = {}
-            for name, ms, b in ops:
-                t = by.setdefault(name, [0.0, 0, 0.0, 0])
-                t[0] += ms
-                t[1] += 1
-                t[2] += b
-                t[3] = b
-            dom = max(by.items(), key=lambda kv: kv[1][0])
-            name, (tot_ms, cnt, _, b_launch) = dom
-            avg_ms = tot_ms / cnt
-            achieved = b_launch / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
-                    "alg_bytes_per_launch": int(b_launch)}
-            extra["kernel_breakdown_ms_per_tile"] = {k: round(v[0], 3) for k, v in by.items()}
+        # the layer-by-layer path (one HBM pass per fused op; the fallback for programs the
+        # whole-network kernel has no instantiation for): its dominant conv kernel against
+        # the HBM roof — the north star's "Conv2d covariance kernel" target
+        with torch.no_grad():
+            ops = probe_kernels(model, X[:B], B, B)
+        by = {}
+        for name, ms, b in ops:
+            t = by.setdefault(name, [0.0, 0, 0.0, 0])
+            t[0] += ms
+            t[1] += 1
+            t[2] += b
+            t[3] = b
+        convs = {k: v for k, v in by.items() if "conv" in k} or by
+        name, (tot_ms, cnt, _, b_launch) = max(convs.items(), key=lambda kv: kv[1][0])
+        avg_ms = tot_ms / cnt
+        achieved = b_launch / (avg_ms * 1e-3) / 1e9
+        layer = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                 "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
+                 "alg_bytes_per_launch": int(b_launch),
+                 "layer_path_tile_ms": round(sum(v[0] for v in by.values()), 3),
+                 "kernel_breakdown_ms_per_tile": {k: round(v[0], 3) for k, v in by.items()}}
+        if roof is None:
+            roof = layer
+        else:
+            extra["layer_path_conv_roofline"] = layer
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
