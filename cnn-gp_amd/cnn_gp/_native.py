@@ -57,7 +57,7 @@ class NetOp(ctypes.Structure):
         ("kind", _i32), ("code", _i32), ("src", _i32), ("dst", _i32), ("add", _i32),
         ("ws_in", _i32), ("ws_out", _i32), ("relu", _i32), ("h", _i32), ("w", _i32),
         ("div_m", ctypes.c_uint32), ("div_s", ctypes.c_uint32),
-        ("dst2", _i32), ("reserved", _i32),
+        ("dst2", _i32), ("zero_halo", _i32),
         ("weight", _f64), ("bias", _f64), ("var_x", _vp), ("var_y", _vp),
         ("var2_x", _vp), ("var2_y", _vp),
     ]

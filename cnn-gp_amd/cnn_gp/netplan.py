@@ -63,6 +63,15 @@ def _conv_halo(op):
     return left, right
 
 
+def _zero_code(z):
+    """cgp_net_op.zero_halo half-word of (HL, gap): 0 = leave the halos alone."""
+    if z is None:
+        return 0
+    hl, gap = z
+    assert 0 <= hl < 256 and 0 < gap < 256
+    return hl << 8 | gap
+
+
 class NetPlan:
     """The whole-network kernel program for one Plan (one model at one input size)."""
 
@@ -124,32 +133,74 @@ class NetPlan:
                 for s in srcs:
                     last[s] = idx
         last[vf] = len(lowered)
-        # 4. slot allocation (linear scan, per class free lists, in-place allowed)
-        free: dict = {}
+        # 4. slot allocation: first fit over one LDS arena after the row-sum scratch, so
+        #    dead slots of one class host values of another (a ResNet's 28x28 slots take
+        #    its 14x14 and 7x7 values).  A value may take the slot of a source that dies
+        #    at its producer when the class matches (in place, same cells); other slots
+        #    of dying values are released only after the producer's output is placed.
         slots: dict = {}
-        top = 0
         self.hs = 0
-        top = (hs_need + ALIGN - 1) // ALIGN * ALIGN
+        arena0 = (hs_need + ALIGN - 1) // ALIGN * ALIGN
+        top = arena0
+        free: list = []                       # sorted disjoint [a, b) element intervals
+        dying: list = []
+        placements: list = []                 # (slot, index of the producer record)
+
+        def take(n):
+            nonlocal top
+            for k, (lo, hi) in enumerate(free):
+                if hi - lo >= n:
+                    if hi - lo == n:
+                        del free[k]
+                    else:
+                        free[k] = (lo + n, hi)
+                    return lo
+            lo = free.pop()[0] if free and free[-1][1] == top else top
+            top = max(top, lo + n)
+            return lo
+
+        def give(lo, n):
+            free.append((lo, lo + n))
+            free.sort()
+            merged = []
+            for iv in free:
+                if merged and merged[-1][1] == iv[0]:
+                    merged[-1] = (merged[-1][0], iv[1])
+                else:
+                    merged.append(iv)
+            free[:] = merged
 
         def alloc(v):
-            nonlocal top
             c = tuple(shapes[v])
-            lst = free.get(c)
-            if lst:
-                sl = lst.pop()
+            for k, dv in enumerate(dying):
+                if slots[dv].cls == c:
+                    sl = slots[dying.pop(k)]
+                    del slots[dv]
+                    break
             else:
-                hl = halo[c][0]
-                sl = _Slot(top, top + hl, c)
-                top += slot_elems(c)
+                base = take(slot_elems(c))
+                sl = _Slot(base, base + halo[c][0], c)
+                # a fresh region: its halos are what the zeroing pass below checks (a
+                # value taking a dying source's slot in place inherits clean halos —
+                # nothing else can write inside a live slot)
+                placements.append((sl, len(recs)))
             slots[v] = sl
             return sl
 
         def release_dead(idx):
-            for v in [v for v, sl in slots.items() if last.get(v, -1) == idx and v != vf]:
-                free.setdefault(slots[v].cls, []).append(slots.pop(v))
+            for v in [v for v in slots if last.get(v, -1) == idx and v != vf]:
+                if v not in dying:
+                    dying.append(v)
+
+        def commit():
+            for dv in dying:
+                sl = slots.pop(dv)
+                give(sl.base, slot_elems(sl.cls))
+            dying.clear()
 
         recs = []           # (NetOp fields dict, var value or None)
         for idx, (kind, a, op) in enumerate(lowered):
+            commit()
             if kind == "moments":
                 h, w = shapes[v0]
                 release_dead(idx)
@@ -203,6 +254,40 @@ class NetPlan:
                     for (c, _), so in zip(terms[2:], srcs[2:]):
                         recs.append((dict(base, src=d.origin, add=so, weight=1.0, bias=c),
                                      None))
+        final_origin = slots[vf].origin
+        commit()
+        # 4b. slot halos must read as zeros.  A fresh placement finds them dirty when,
+        #     since the previous placement of the same slot (cyclically: the program
+        #     repeats for every pair of the workgroup), another placement wrote data on
+        #     them; such a slot is cleared by a ZERO op before its producer
+        cells = {}
+        for sl, _ in placements:
+            key = (sl.base, sl.cls)
+            if key not in cells:
+                h_, w_ = sl.cls
+                ws_ = self.ws[sl.cls]
+                data = {sl.origin + r * ws_ + q for r in range(h_) for q in range(w_)}
+                cells[key] = (data, set(range(sl.base, sl.base + slot_elems(sl.cls))) - data)
+        zero_at = {}
+        npl = len(placements)
+        for t, (sl, ri) in enumerate(placements):
+            if max(halo[sl.cls]) == 0:
+                continue                      # no conv reads beyond this class's data
+            key = (sl.base, sl.cls)
+            halo_cells = cells[key][1]
+            for back in range(1, npl + 1):
+                sl2 = placements[(t - back) % npl][0]
+                key2 = (sl2.base, sl2.cls)
+                if key2 == key:
+                    break
+                if halo_cells & cells[key2][0]:
+                    zero_at.setdefault(ri, []).append(sl)
+                    break
+        for ri, sls in zero_at.items():
+            assert len(sls) == 1
+            sl = sls[0]
+            recs[ri][0]["zero"] = (halo[sl.cls][0], self.ws[sl.cls] - sl.cls[1])
+        self.n_zero = sum(len(v) for v in zero_at.values())
         # 5. dual outputs: a standalone ReLU of the value the previous op just produced
         #    (a residual block's relu(x) branch input) is written by that op's output
         #    stage as a second result, saving an op, a barrier and an LDS round trip
@@ -216,6 +301,8 @@ class NetPlan:
                         and prev["dst"] == f["src"] and (prev["h"], prev["w"]) == (f["h"], f["w"])):
                     prev["dst2"] = f["dst"]
                     prev["var2"] = v
+                    if "zero" in f:
+                        prev["zero2"] = f["zero"]
                     continue
                 folded.append((f, v))
             recs = folded
@@ -224,7 +311,7 @@ class NetPlan:
                 f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
             elif f["kind"] != N.CGP_NET_CONV:
                 f["code"] = -1
-        self.final_slot = slots[vf].origin
+        self.final_slot = final_origin
         self.hs = 0
         self.lds_elems = top
         self.records = recs
@@ -251,6 +338,7 @@ class NetPlan:
             o.div_m, o.div_s = N.make_fastdiv(f["w"])
             o.weight, o.bias = f.get("weight", 0.0), f.get("bias", 0.0)
             o.dst2 = f.get("dst2", -1)
+            o.zero_halo = _zero_code(f.get("zero")) | (_zero_code(f.get("zero2")) << 16)
             if v is not None:
                 vx, vy = var[v]
                 o.var_x, o.var_y = vx.data_ptr(), vy.data_ptr()

@@ -28,7 +28,10 @@ using namespace cgp;
 
 namespace {
 
-constexpr int kNT = 128;        // threads per workgroup: two waves per pair
+#ifndef CGP_NET_NT
+#define CGP_NET_NT 128
+#endif
+constexpr int kNT = CGP_NET_NT;  // threads per workgroup (one pair): two waves
 #ifndef CGP_NET_STL
 #define CGP_NET_STL 3
 #endif
@@ -305,7 +308,10 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if ((tid & 63) == 0) part[tid >> 6] = acc;
         lds_barrier();
         if (tid == 0) {
-            T v[1] = {fma_t(w, part[0] + part[1], b)};
+            T tot = part[0];
+#pragma unroll
+            for (int k = 1; k < kNT / 64; ++k) tot += part[k];
+            T v[1] = {fma_t(w, tot, b)};
             const int at[1] = {0};
             const bool ok[1] = {true};
             T u1[1] = {T(1)}, u2[1] = {T(1)};
@@ -499,6 +505,26 @@ __device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& 
     }
 }
 
+// Zero the halo cells of the slot whose pixel (0, 0) is at `origin` (code = (HL << 8) |
+// gap, see cgp_net_op.zero_halo): HL cells before it and `gap` after each of the h rows.
+// Disjoint from every data cell, so it needs no barrier against the op's own writes.
+template <typename T>
+__device__ __forceinline__ void zero_halos(T* lds, int origin, int code, int h, int w, int ws,
+                                           int tid) {
+    if (!code) return;
+    const int hl = code >> 8, gap = code & 0xff;
+    for (int e = tid; e < hl + h * gap; e += kNT) {
+        int cell;
+        if (e < hl) {
+            cell = origin - hl + e;
+        } else {
+            const int r = (e - hl) / gap;
+            cell = origin + r * ws + w + (e - hl - r * gap);
+        }
+        lds[cell] = T(0);
+    }
+}
+
 // pair walk: supertile s (kST x kST pairs) -> (bi, bj); same tiles enumerate the upper
 // triangle (bi <= bj) row-major
 __device__ __forceinline__ void tri_decode(unsigned s, unsigned nb, unsigned& bi,
@@ -584,6 +610,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         for (int k = 0; k < p.nops; ++k) {
             const cgp_net_op op = p.ops[k];
+            if (op.zero_halo) {
+                zero_halos(lds, op.dst, op.zero_halo & 0xffff, op.h, op.w, op.ws_out, tid);
+                zero_halos(lds, op.dst2, (unsigned)op.zero_halo >> 16, op.h, op.w, op.ws_out,
+                           tid);
+            }
             switch (op.kind) {
             case CGP_NET_CONV:
                 switch (op.code) {
@@ -601,6 +632,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
             case CGP_NET_LINEAR:
                 net_elem_dispatch<T, EX, DU, CGP_NET_LINEAR>(lds, op, p, i, j);
                 break;
+
             default:
                 break;
             }
@@ -615,11 +647,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-// waves per SIMD the LDS footprint allows (2 waves per workgroup, 4 SIMDs per CU),
+// waves per SIMD the LDS footprint allows (kNT / 64 waves per workgroup, 4 SIMDs per CU),
 // clamped to the instantiated register targets 3..5
 inline int net_wpe(long long lds_bytes) {
     const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
-    const long long w = wg / 2;
+    const long long w = wg * (kNT / 64) / 4;
     return w < 3 ? 3 : (w > 5 ? 5 : (int)w);
 }
 

@@ -226,7 +226,12 @@ typedef struct cgp_net_op {
     int32_t h, w;          /* RELU / LINEAR / MOMENTS: map size (CONV: output size) */
     uint32_t div_m, div_s; /* w as a multiply-high divisor (host: make_fastdiv(w)) */
     int32_t dst2;          /* CONV/RELU/LINEAR: also write relu(result) here (< 0: no) */
-    int32_t reserved;
+    int32_t zero_halo;     /* before the op, zero the halo cells of the dst slot (bits 0-15)
+                              and of the dst2 slot (bits 16-31), each (HL << 8) | gap:
+                              HL cells before pixel (0, 0) and `gap` = ws_out - w cells
+                              after every row; 0 = none.  Set on a slot placed on cells
+                              another slot used as data (the LDS arena is shared across
+                              map sizes). */
     double weight, bias;   /* CONV: w·Σ + b;  LINEAR: dst = weight·src + bias·add */
     const void* var_x;     /* ReLU input variances of the x images, [n1][h·w] */
     const void* var_y;     /* ... of the y images, [n2][h·w] */

@@ -65,8 +65,12 @@ def _relu(c, v1, v2):
         return (sin + (math.pi - np.arccos(cos)) * c) / (2 * math.pi)
 
 
-def run_pair(net, x_i, y_j, var, i, j):
-    lds = np.zeros(net.lds_elems)
+def run_pair(net, x_i, y_j, var, i, j, lds=None):
+    """One pair through the op list.  ``lds`` persists across the pairs of a workgroup
+    (the kernel zeroes it once per workgroup), so stale values of earlier pairs stay in
+    every cell an op does not write — as on the device."""
+    if lds is None:
+        lds = np.zeros(net.lds_elems)
     hs0 = net.hs
 
     def plane(off, h, w, ws):
@@ -75,6 +79,13 @@ def run_pair(net, x_i, y_j, var, i, j):
 
     for f, v in net.records:
         kind = f["kind"]
+        for key, dst in (("zero", f["dst"]), ("zero2", f.get("dst2", -1))):
+            if key in f:                                        # cgp_net_op.zero_halo
+                hl, gap = f[key]
+                lds[dst - hl:dst] = 0.0
+                for r in range(f["h"]):
+                    c0 = dst + r * f["ws_out"] + f["w"]
+                    lds[c0:c0 + gap] = 0.0
         if kind == 2:                                           # MOMENTS
             h, w = f["h"], f["w"]
             C = x_i.shape[0]
@@ -128,6 +139,7 @@ def kernel(net, x, y, same):
     var = variances(net.plan, x, y)
     n1, n2 = x.shape[0], y.shape[0]
     K = np.zeros((n1, n2))
+    lds = np.zeros(net.lds_elems)           # one workgroup walks every pair
     for i in range(n1):
         for j in range(n2):
             if same and i == j:
@@ -135,5 +147,5 @@ def kernel(net, x, y, same):
             elif same and j < i:
                 K[i, j] = K[j, i]
             else:
-                K[i, j] = run_pair(net, x[i], y[j], var, i, j)
+                K[i, j] = run_pair(net, x[i], y[j], var, i, j, lds)
     return K
