@@ -14,13 +14,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 3
+CGP_ABI_VERSION = 4
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
 CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
 CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
+CGP_NET_LOAD, CGP_NET_STORE = 4, 5
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -70,7 +71,8 @@ class NetArgs(ctypes.Structure):
         ("n1", _i64), ("n2", _i64), ("ldo", _i64),
         ("nops", _i32), ("channels", _i32), ("h", _i32), ("w", _i32),
         ("same", _i32), ("final_slot", _i32), ("hs", _i32), ("lds_elems", _i32),
-        ("flags", _i32), ("reserved", _i32),
+        ("flags", _i32), ("pairs", _i32), ("unit_begin", _i64), ("unit_end", _i64),
+        ("final_stage", _i32), ("reserved2", _i32),
     ]
 
 
@@ -114,7 +116,7 @@ SIGNATURES = {
     "cgp_net_resolution": (_i32, [_i32, _i32]),
     "cgp_net_op_size": (ctypes.c_size_t, []),
     "cgp_net_args_size": (ctypes.c_size_t, []),
-    "cgp_net_occupancy": (_i32, [_i32, _i32, _i32]),
+    "cgp_net_occupancy": (_i32, [_i32, _i32, _i32, _i32]),
     "cgp_net_f64": (_i32, [ctypes.POINTER(NetArgs), _vp]),
     "cgp_net_f32": (_i32, [ctypes.POINTER(NetArgs), _vp]),
 }

@@ -72,16 +72,50 @@ def _zero_code(z):
     return hl << 8 | gap
 
 
-class NetPlan:
-    """The whole-network kernel program for one Plan (one model at one input size)."""
+@dataclasses.dataclass
+class Stage:
+    """One launch of the whole-network kernel: a contiguous run of the lowered program
+    with its own LDS arena (per pair) and pairs per workgroup."""
+    records: list
+    lds_elems: int
+    final_slot: int
+    pairs: int
+    final: bool
+    load_stride: int                   # elements per unit of the incoming state record
+    store_stride: int                  # ... of the outgoing one
 
-    def __init__(self, plan, itemsize: int = 8, dual: bool = True):
+    @property
+    def n_ops(self):
+        return len(self.records)
+
+    @property
+    def dual(self):
+        return any(f.get("dst2", -1) >= 0 for f, _ in self.records)
+
+
+# pairs per workgroup of a stage whose maps are all at most this many pixels
+MULTI_PAIR = ((16, 64), (4, 256))
+MIN_STAGE_OPS = 4                      # a shorter tail is not worth a launch + state
+CHUNK_BYTES = 1 << 30                  # state buffers: units per launch group
+
+
+class NetPlan:
+    """The whole-network kernel program for one Plan (one model at one input size).
+
+    The program is lowered to one or more stages.  A network whose tail runs on small
+    maps (a ResNet's 14x14 and 7x7 blocks) is split where the maps drop to <= 16x16 and
+    <= 8x8: those stages run 4 and 16 pairs per workgroup (csrc/netfuse.hip), so a small
+    map's op still fills the workgroup's 128 threads.  The maps live across a boundary
+    cross it through a per-unit state buffer (CGP_NET_STORE / CGP_NET_LOAD)."""
+
+    def __init__(self, plan, itemsize: int = 8, dual: bool = True, stages: bool = True):
         self.plan = plan
         prog, v0, vf = plan.prog, plan.v0, plan.vf
         if plan.final_hw != (1, 1):
             raise Unsupported(f"final map is {plan.final_hw}, not 1x1")
         ops = fuse(prog, v0, vf, True, pre_relu=False, fold_moments=False)
         lib = N.load()
+        self._lib = lib
         # 1. per-op checks + geometry codes
         hs_need = 2
         codes = {}
@@ -101,8 +135,10 @@ class NetPlan:
                 pass
             else:
                 raise Unsupported(f"op {op.kind}")
+        self._codes = codes
         # 2. slot classes and their halos
         shapes = prog.shapes
+        self._shapes = shapes
         halo = {}
         for v, shp in shapes.items():
             halo.setdefault(tuple(shp), [0, 0])
@@ -112,55 +148,159 @@ class NetPlan:
                 hl = halo[tuple(op.shape_in)]
                 hl[0] = max(hl[0], lft)
                 hl[1] = max(hl[1], rgt)
+        self._halo = halo
         # rows share their zero gap: row r's right halo and row r+1's left halo are the
         # same max(HL, HR) columns; the slot adds HL before row 0 and HR after the last
         self.ws = {c: c[1] + max(hl) for c, hl in halo.items()}
+        # 3. a linear op list: the moments, then the fused ops
+        lowered = [("moments", v0, None)]
+        for k, op in enumerate(ops):
+            lowered.append(("op", k, op))
+        last = {}
+        prod = {v0: 0}
+        for idx, (kind, a, op) in enumerate(lowered):
+            if kind == "op":
+                prod[op.dst] = idx
+                for s_ in self._sources(op):
+                    last[s_] = idx
+        last[vf] = len(lowered)
+        # 4. stages, then each stage's slots and records
+        multi = stages and itemsize == 8 and not plan.flags & N.CGP_FLAG_EXACT_RELU
+        bounds = self._stage_bounds(lowered, multi)
+        self.stages = []
+        for sidx, (lo, hi, np_) in enumerate(bounds):
+            ins = sorted(v for v, pi in prod.items() if pi < lo and last.get(v, -1) >= lo)
+            outs = sorted(v for v, pi in prod.items() if pi < hi <= last.get(v, -1)) \
+                if hi < len(lowered) else []
+            self.stages.append(self._lower(lowered, lo, hi, np_, ins, outs, last, dual,
+                                           itemsize))
+        self.need_var = {vf}
+        for st in self.stages:
+            self.need_var |= {v for _, v in st.records if v is not None}
+            self.need_var |= {f["var2"] for f, _ in st.records if "var2" in f}
+
+    # -- compatibility view of a one-stage program -----------------------------------------
+    @property
+    def records(self):
+        return [r for st in self.stages for r in st.records]
+
+    @property
+    def lds_elems(self):
+        return max(st.lds_elems * st.pairs for st in self.stages)
+
+    @property
+    def final_slot(self):
+        return self.stages[-1].final_slot
+
+    @property
+    def dual(self):
+        return any(st.dual for st in self.stages)
+
+    @property
+    def n_ops(self):
+        return sum(st.n_ops for st in self.stages)
+
+    hs = 0
+
+    @staticmethod
+    def _sources(op):
+        srcs = ([op.src] if op.src is not None else []) + [t for _, t in op.terms]
+        if op.addend is not None:
+            srcs.append(op.addend)
+        return srcs
+
+    def _stage_bounds(self, lowered, multi):
+        """[(lo, hi, pairs)]: one stage, or the network split where every later op's maps
+        fit 4 / 16 pairs per workgroup (compile-time sizes only)."""
+        n = len(lowered)
+        if not multi:
+            return [(0, n, 1)]
+        lib, shapes = self._lib, self._shapes
+        inf = 1 << 30
+
+        def px(idx):
+            kind, _, op = lowered[idx]
+            if kind == "moments":
+                return inf
+            vals = [op.dst] + self._sources(op)
+            if op.kind in ("relu", "add"):
+                h, w = shapes[op.dst]
+                if lib.cgp_net_resolution(h, w) < 0:
+                    return inf
+            return max(shapes[v][0] * shapes[v][1] for v in vals)
+
+        smax = [0] * (n + 1)
+        for idx in range(n - 1, -1, -1):
+            smax[idx] = max(px(idx), smax[idx + 1])
+        cuts = []
+        for pairs, lim in MULTI_PAIR:
+            k = next((idx for idx in range(1, n) if smax[idx] <= lim), n)
+            cuts.append((k, pairs))
+        k16, k4 = cuts[0][0], cuts[1][0]
+        bounds = []
+        edges = [(0, 1)]
+        if k4 < k16:
+            edges.append((k4, 4))
+        if k16 < n:
+            edges.append((k16, 16))
+        # a multi-pair stage shorter than MIN_STAGE_OPS stays with its predecessor
+        kept = [edges[0]]
+        for k, pairs in edges[1:]:
+            nxt = next((k2 for k2, _ in edges if k2 > k), n)
+            if nxt - k >= MIN_STAGE_OPS:
+                kept.append((k, pairs))
+        for t, (k, pairs) in enumerate(kept):
+            hi = kept[t + 1][0] if t + 1 < len(kept) else n
+            bounds.append((k, hi, pairs))
+        return bounds
+
+    def _lower(self, lowered, lo, hi, pairs, ins, outs, last, dual, itemsize):
+        """Slots and records of lowered[lo:hi] (inputs loaded from the incoming state
+        record, outputs stored to the outgoing one)."""
+        lib, shapes, halo = self._lib, self._shapes, self._halo
+        plan = self.plan
+        v0, vf = plan.v0, plan.vf
+        final = hi == len(lowered)
 
         def slot_elems(c):
             n = halo[c][0] + c[0] * self.ws[c] + halo[c][1]
             return (n + ALIGN - 1) // ALIGN * ALIGN
 
-        # 3. lower to a linear op list with explicit LINEAR chains
-        lowered = [("moments", v0, None)]
-        for k, op in enumerate(ops):
-            lowered.append(("op", k, op))
-        last = {}
-        for idx, (kind, a, op) in enumerate(lowered):
-            if kind == "op":
-                srcs = ([op.src] if op.src is not None else []) + [t for _, t in op.terms]
-                if op.addend is not None:
-                    srcs.append(op.addend)
-                for s in srcs:
-                    last[s] = idx
-        last[vf] = len(lowered)
-        # 4. slot allocation: first fit over one LDS arena after the row-sum scratch, so
-        #    dead slots of one class host values of another (a ResNet's 28x28 slots take
-        #    its 14x14 and 7x7 values).  A value may take the slot of a source that dies
-        #    at its producer when the class matches (in place, same cells); other slots
-        #    of dying values are released only after the producer's output is placed.
+        # last use inside this stage: an output is read by its STORE at index hi
+        last_s = {v: (hi if v in outs else min(u, hi)) for v, u in last.items()}
+        # slot allocation: first fit over one LDS arena after the row-sum scratch, so
+        # dead slots of one class host values of another (a ResNet's 28x28 slots take its
+        # 14x14 and 7x7 values).  A value may take the slot of a source that dies at its
+        # producer when the class matches (in place, same cells); other slots of dying
+        # values are released only after the producer's output is placed.
         slots: dict = {}
-        self.hs = 0
+        hs_need = 2                           # the row-sum scratch this stage's convs need
+        for idx in range(lo, hi):
+            kind, a, op = lowered[idx]
+            if kind == "op" and op.kind == "conv":
+                hs_need = max(hs_need, lib.cgp_net_hs_elems(self._codes[a]))
         arena0 = (hs_need + ALIGN - 1) // ALIGN * ALIGN
         top = arena0
         free: list = []                       # sorted disjoint [a, b) element intervals
         dying: list = []
         placements: list = []                 # (slot, index of the producer record)
+        recs = []                             # (NetOp fields dict, var value or None)
 
         def take(n):
             nonlocal top
-            for k, (lo, hi) in enumerate(free):
-                if hi - lo >= n:
-                    if hi - lo == n:
+            for k, (a_, b_) in enumerate(free):
+                if b_ - a_ >= n:
+                    if b_ - a_ == n:
                         del free[k]
                     else:
-                        free[k] = (lo + n, hi)
-                    return lo
-            lo = free.pop()[0] if free and free[-1][1] == top else top
-            top = max(top, lo + n)
-            return lo
+                        free[k] = (a_ + n, b_)
+                    return a_
+            a_ = free.pop()[0] if free and free[-1][1] == top else top
+            top = max(top, a_ + n)
+            return a_
 
-        def give(lo, n):
-            free.append((lo, lo + n))
+        def give(a_, n):
+            free.append((a_, a_ + n))
             free.sort()
             merged = []
             for iv in free:
@@ -188,7 +328,7 @@ class NetPlan:
             return sl
 
         def release_dead(idx):
-            for v in [v for v in slots if last.get(v, -1) == idx and v != vf]:
+            for v in [v for v in slots if last_s.get(v, -1) == idx and v != vf]:
                 if v not in dying:
                     dying.append(v)
 
@@ -198,8 +338,18 @@ class NetPlan:
                 give(sl.base, slot_elems(sl.cls))
             dying.clear()
 
-        recs = []           # (NetOp fields dict, var value or None)
-        for idx, (kind, a, op) in enumerate(lowered):
+        # stage inputs
+        load_stride = sum(shapes[v][0] * shapes[v][1] for v in ins)
+        off = 0
+        for v in ins:
+            h, w = shapes[v]
+            d = alloc(v)
+            recs.append((dict(kind=N.CGP_NET_LOAD, src=0, dst=d.origin, add=off,
+                              ws_in=self.ws[(h, w)], ws_out=self.ws[(h, w)], h=h, w=w,
+                              code=load_stride, state="in"), None))
+            off += h * w
+        for idx in range(lo, hi):
+            kind, a, op = lowered[idx]
             commit()
             if kind == "moments":
                 h, w = shapes[v0]
@@ -211,13 +361,13 @@ class NetPlan:
                 continue
             k = a
             if op.kind == "conv":
-                s = slots[op.src]
+                s_ = slots[op.src]
                 ad = slots[op.addend].origin if op.addend is not None else -1
                 release_dead(idx)
                 d = alloc(op.dst)
                 ho, wo = op.shape_out
                 relu = op.post == N.CGP_POST_RELU
-                recs.append((dict(kind=N.CGP_NET_CONV, code=codes[k], src=s.origin,
+                recs.append((dict(kind=N.CGP_NET_CONV, code=self._codes[k], src=s_.origin,
                                   dst=d.origin, add=ad, ws_in=self.ws[tuple(op.shape_in)],
                                   ws_out=self.ws[(ho, wo)], relu=int(relu), h=ho, w=wo,
                                   weight=op.geom.weight, bias=op.geom.bias,
@@ -225,12 +375,12 @@ class NetPlan:
                                         op.geom.offset)),
                              op.post_var if relu else None))
             elif op.kind == "relu":
-                s = slots[op.src]
+                s_ = slots[op.src]
                 ad = slots[op.addend].origin if op.addend is not None else -1
                 release_dead(idx)
                 d = alloc(op.dst)
                 h, w = op.shape_out
-                recs.append((dict(kind=N.CGP_NET_RELU, src=s.origin, dst=d.origin, add=ad,
+                recs.append((dict(kind=N.CGP_NET_RELU, src=s_.origin, dst=d.origin, add=ad,
                                   ws_in=self.ws[(h, w)], ws_out=self.ws[(h, w)], relu=1,
                                   h=h, w=w), op.src))
             else:   # add: dst = c0·t0 + c1·t1, then dst = dst + c_k·t_k
@@ -254,12 +404,21 @@ class NetPlan:
                     for (c, _), so in zip(terms[2:], srcs[2:]):
                         recs.append((dict(base, src=d.origin, add=so, weight=1.0, bias=c),
                                      None))
-        final_origin = slots[vf].origin
         commit()
-        # 4b. slot halos must read as zeros.  A fresh placement finds them dirty when,
-        #     since the previous placement of the same slot (cyclically: the program
-        #     repeats for every pair of the workgroup), another placement wrote data on
-        #     them; such a slot is cleared by a ZERO op before its producer
+        # stage outputs
+        store_stride = sum(shapes[v][0] * shapes[v][1] for v in outs)
+        off = 0
+        for v in outs:
+            h, w = shapes[v]
+            recs.append((dict(kind=N.CGP_NET_STORE, src=slots[v].origin, dst=0, add=off,
+                              ws_in=self.ws[(h, w)], ws_out=self.ws[(h, w)], h=h, w=w,
+                              code=store_stride, state="out"), None))
+            off += h * w
+        final_origin = slots[vf].origin if final else 0
+        # halo zeroing: slot halos must read as zeros.  A fresh placement finds them dirty
+        # when, since the previous placement of the same slot (cyclically: the stage's
+        # ops repeat for every pair of the workgroup), another placement wrote data on
+        # them; its producer then zeroes the halo cells first
         cells = {}
         for sl, _ in placements:
             key = (sl.base, sl.cls)
@@ -268,7 +427,6 @@ class NetPlan:
                 ws_ = self.ws[sl.cls]
                 data = {sl.origin + r * ws_ + q for r in range(h_) for q in range(w_)}
                 cells[key] = (data, set(range(sl.base, sl.base + slot_elems(sl.cls))) - data)
-        zero_at = {}
         npl = len(placements)
         for t, (sl, ri) in enumerate(placements):
             if max(halo[sl.cls]) == 0:
@@ -281,16 +439,11 @@ class NetPlan:
                 if key2 == key:
                     break
                 if halo_cells & cells[key2][0]:
-                    zero_at.setdefault(ri, []).append(sl)
+                    recs[ri][0]["zero"] = (halo[sl.cls][0], self.ws[sl.cls] - sl.cls[1])
                     break
-        for ri, sls in zero_at.items():
-            assert len(sls) == 1
-            sl = sls[0]
-            recs[ri][0]["zero"] = (halo[sl.cls][0], self.ws[sl.cls] - sl.cls[1])
-        self.n_zero = sum(len(v) for v in zero_at.values())
-        # 5. dual outputs: a standalone ReLU of the value the previous op just produced
-        #    (a residual block's relu(x) branch input) is written by that op's output
-        #    stage as a second result, saving an op, a barrier and an LDS round trip
+        # dual outputs: a standalone ReLU of the value the previous op just produced (a
+        # residual block's relu(x) branch input) is written by that op's output stage as
+        # a second result, saving an op, a barrier and an LDS round trip
         if dual:
             folded = []
             for f, v in recs:
@@ -307,27 +460,22 @@ class NetPlan:
                 folded.append((f, v))
             recs = folded
         for f, _ in recs:
-            if f["kind"] == N.CGP_NET_RELU:
+            if f["kind"] == N.CGP_NET_RELU or (f["kind"] == N.CGP_NET_LINEAR and pairs > 1):
                 f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
-            elif f["kind"] != N.CGP_NET_CONV:
+            elif f["kind"] in (N.CGP_NET_MOMENTS, N.CGP_NET_LINEAR):
                 f["code"] = -1
-        self.final_slot = final_origin
-        self.hs = 0
-        self.lds_elems = top
-        self.records = recs
-        self.dual = any(f.get("dst2", -1) >= 0 for f, _ in recs)
-        self.need_var = {v for _, v in recs if v is not None} | {vf} | \
-            {f["var2"] for f, _ in recs if "var2" in f}
-        self.n_ops = len(recs)
-        if self.lds_elems * itemsize > MAX_LDS_BYTES:
-            raise Unsupported(f"LDS footprint {self.lds_elems * itemsize} B")
+        if top * itemsize * pairs > MAX_LDS_BYTES:
+            if pairs == 1:
+                raise Unsupported(f"LDS footprint {top * itemsize} B")
+        return Stage(records=recs, lds_elems=top, final_slot=final_origin, pairs=pairs,
+                     final=final, load_stride=load_stride, store_stride=store_stride)
 
     def lds_bytes(self, itemsize: int) -> int:
         return self.lds_elems * itemsize
 
-    def _ops_array(self, var):
-        arr = (N.NetOp * self.n_ops)()
-        for k, (f, v) in enumerate(self.records):
+    def _ops_array(self, stage, var, state_in=None, state_out=None):
+        arr = (N.NetOp * stage.n_ops)()
+        for k, (f, v) in enumerate(stage.records):
             o = arr[k]
             o.kind = f["kind"]
             o.code = f.get("code", 0)
@@ -345,47 +493,81 @@ class NetPlan:
             if "var2" in f:
                 vx, vy = var[f["var2"]]
                 o.var2_x, o.var2_y = vx.data_ptr(), vy.data_ptr()
+            if f.get("state") == "in":
+                o.var_x = state_in.data_ptr()
+            elif f.get("state") == "out":
+                o.var_x = state_out.data_ptr()
         return arr
+
+    @staticmethod
+    def units(n1: int, n2: int, same: bool) -> int:
+        """Pair units of a tile: 8x8 supertiles (upper triangle when same) x 64."""
+        nbi, nbj = -(-n1 // 8), -(-n2 // 8)
+        return (nbi * (nbi + 1) // 2 if same else nbi * nbj) * 64
 
     def prepare(self, x, y, var, n1: int, n2: int, same: bool, flags: int = 0,
                 out: Optional[torch.Tensor] = None):
-        """Upload the op list for these variance maps; return (launch(stream), out).
+        """Upload the op lists for these variance maps; return (launch(stream), out).
         ``out`` may be a row-strided view (e.g. a tile of a larger K): the kernel writes
         K[i, j] at out[i * out.stride(0) + j]."""
         sfx = "f64" if x.dtype == torch.float64 else "f32"
-        arr = self._ops_array(var)
-        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-        ops_dev = host.to(x.device)                 # stream-ordered, freed stream-ordered
         if out is None:
             out = torch.empty((n1, n2), dtype=x.dtype, device=x.device)
         if out.shape != (n1, n2) or out.stride(1) != 1 or out.dtype != x.dtype:
             raise ValueError("out must be an [n1, n2] row-major view of the input dtype")
-        a = N.NetArgs()
-        a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
-        if same:
-            kd = var[self.plan.vf][0]
-            a.kdiag = kd.data_ptr()
-        a.ops = ops_dev.data_ptr()
-        a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
-        a.nops, a.channels, a.h, a.w = self.n_ops, x.shape[1], x.shape[2], x.shape[3]
-        a.same, a.final_slot, a.hs, a.lds_elems = int(same), self.final_slot, self.hs, \
-            self.lds_elems
-        a.flags = flags | (N.CGP_FLAG_NET_DUAL if self.dual else 0)
+        units = self.units(n1, n2, same)
+        multi = len(self.stages) > 1
+        chunk = units
+        states = [None] * (len(self.stages) + 1)
+        if multi:
+            stride = max(max(st.load_stride, st.store_stride) for st in self.stages)
+            chunk = max(64, CHUNK_BYTES // (stride * x.element_size()) // 64 * 64)
+            chunk = min(chunk, units)
+            for b in range(1, len(self.stages)):
+                states[b] = torch.empty((chunk * self.stages[b].load_stride,),
+                                        dtype=x.dtype, device=x.device)
         fn = getattr(N.load(), f"cgp_net_{sfx}")
+        launches = []
+        keep = []
+        for sidx, st in enumerate(self.stages):
+            arr = self._ops_array(st, var, states[sidx], states[sidx + 1])
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            ops_dev = host.to(x.device)             # stream-ordered, freed stream-ordered
+            keep.append(ops_dev)
+            a = N.NetArgs()
+            a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
+            if same:
+                a.kdiag = var[self.plan.vf][0].data_ptr()
+            a.ops = ops_dev.data_ptr()
+            a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
+            a.nops, a.channels, a.h, a.w = st.n_ops, x.shape[1], x.shape[2], x.shape[3]
+            a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, 0, st.lds_elems
+            a.flags = flags | (N.CGP_FLAG_NET_DUAL if st.dual else 0)
+            a.pairs = st.pairs
+            a.final_stage = int(st.final)
+            launches.append(a)
 
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2
 
-        def launch(stream, a=a, ops_dev=ops_dev, fn=fn):
+        def run_all(stream):
+            for u0 in range(0, units, chunk):
+                u1 = min(units, u0 + chunk)
+                for a in launches:
+                    if multi:
+                        a.unit_begin, a.unit_end = u0, u1
+                    N.check(fn(ctypes.byref(a), stream), "cgp_net")
+
+        def launch(stream, keep=keep, states=states):
             if TIMING is not None:
-                st = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+                st_ = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(st)
-                N.check(fn(ctypes.byref(a), stream), "cgp_net")
-                e1.record(st)
+                e0.record(st_)
+                run_all(stream)
+                e1.record(st_)
                 TIMING.append((e0, e1, pairs))
             else:
-                N.check(fn(ctypes.byref(a), stream), "cgp_net")
+                run_all(stream)
 
         return launch, out
 

@@ -57,9 +57,11 @@ constexpr int pick_r(int lines, int len, int taps, int s, int epi) {
     return best;
 }
 
-template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_>
+// NP_: pairs per workgroup (their items share the passes; per-pair counts below)
+template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_, int NP_ = 1>
 struct NG {
     static constexpr int H = H_, W = W_, HO = HO_, WO = WO_, TAPS = TAPS_, S = S_, OFF = OFF_;
+    static constexpr int NP = NP_;
     static constexpr int HW = H * W, HOWO = HO * WO;
     static constexpr bool POINT = TAPS == 1 && OFF == 0;
     static constexpr bool REDUCE = HO == 1 && WO == 1 && OFF == 0 && TAPS == H && TAPS == W;
@@ -67,11 +69,11 @@ struct NG {
     static constexpr int Q0 = OFF < 0 ? -OFF : 0;              // first hs row backed by input
     static constexpr int Q1 = HSR < H - OFF ? HSR : H - OFF;   // one past the last
     static constexpr int NVR = Q1 - Q0;                        // input rows the row pass reads
-    static constexpr int R2 = pick_r(NVR, WO, TAPS, S, 2);
-    static constexpr int R3 = pick_r(WO, HO, TAPS, S, 8);
+    static constexpr int R2 = pick_r(NVR * NP, WO, TAPS, S, 2);
+    static constexpr int R3 = pick_r(WO * NP, HO, TAPS, S, 8);
     static constexpr int WIN2 = (R2 - 1) * S + TAPS, WIN3 = (R3 - 1) * S + TAPS;
-    static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NH + kNT - 1) / kNT;
-    static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NV + kNT - 1) / kNT;
+    static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NP * NH + kNT - 1) / kNT;
+    static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NP * NV + kNT - 1) / kNT;
     static constexpr int NZ = (HSR - NVR) * WO;                // zero cells of hs
     static constexpr int HS_ELEMS = (POINT || REDUCE) ? 2 : HSR * WO;
 };
@@ -194,10 +196,29 @@ struct NetP {
     T* __restrict__ out;
     const T* __restrict__ kdiag;
     const cgp_net_op* __restrict__ ops;
-    long long ldo, units;
+    long long ldo, units, ubeg, uend;
     unsigned n1, n2, nbi, nbj;
-    int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact;
+    int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact, final_stage;
 };
+
+// The pairs an op works on.  NP == 1: (i, j), uniform.  NP > 1: pair q of the group is
+// (tab[q], tab[kMaxNP + q]) from the workgroup's pair table in LDS, unit u0 + q.
+constexpr int kMaxNP = 16;
+struct Pairs {
+    unsigned i, j;
+    const unsigned* tab;
+    long long u0;
+};
+template <int NP>
+__device__ __forceinline__ void pair_q(const Pairs& pr, int q, unsigned& iq, unsigned& jq) {
+    if constexpr (NP == 1) {
+        iq = pr.i;
+        jq = pr.j;
+    } else {
+        iq = pr.tab[q];
+        jq = pr.tab[kMaxNP + q];
+    }
+}
 
 // EXACT (CGP_FLAG_EXACT_RELU) is a separate instantiation: a call to the out-of-line
 // relu_exact would make every register live across it caller-saved
@@ -282,17 +303,30 @@ __device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, u
 }
 
 // ---- CGP_NET_CONV -------------------------------------------------------------------
+// G::NP pairs: item it of a pass belongs to pair q = it / (items per pair) and works on
+// that pair's LDS arena (q · lds_elems) and variance maps.
 template <typename T, bool EX, bool DU, class G>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
-                                         const NetP<T>& p, unsigned i, unsigned j) {
+                                         const NetP<T>& p, const Pairs& pr) {
+    constexpr int NP = G::NP;
     const int tid = opaque_tid();
     const PolyTab tab = poly_table();
     const T w = T(op.weight), b = T(op.bias);
-    const VarSrc<T> vs = var_src<T>(op, i, j, G::HOWO);
+    const int arena = NP == 1 ? 0 : p.lds_elems;
+    const VarSrc<T> vs0 = var_src<T>(op, pr.i, pr.j, G::HOWO);   // NP == 1
+    auto vs_of = [&](int q) {
+        if constexpr (NP == 1) {
+            return vs0;
+        } else {
+            unsigned iq, jq;
+            pair_q<NP>(pr, q, iq, jq);
+            return var_src<T>(op, iq, jq, G::HOWO);
+        }
+    };
     const T* __restrict__ src = lds + op.src;
     const int wsi = op.ws_in, wso = op.ws_out;
 
-    if constexpr (G::REDUCE) {
+    if constexpr (G::REDUCE && NP == 1) {
         // 1x1 output from a full-plane window: a block reduction
         T acc = T(0);
 #pragma unroll
@@ -315,6 +349,36 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             const int at[1] = {0};
             const bool ok[1] = {true};
             T u1[1] = {T(1)}, u2[1] = {T(1)};
+            if (vs0.on) {
+                u1[0] = vs0.x[0];
+                u2[0] = vs0.y[0];
+            }
+            net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
+        }
+    } else if constexpr (G::REDUCE) {
+        // NP pairs: kNT / NP lanes per pair (within one wave) sum its map, then a
+        // segmented butterfly; the group's first lane finishes the pair
+        constexpr int TPP = kNT / NP;
+        static_assert(TPP <= 64 && kNT % NP == 0, "reduce groups must not straddle waves");
+        const int q = tid / TPP, lane = tid - q * TPP;
+        const T* srcq = src + q * arena;
+        T acc = T(0);
+#pragma unroll
+        for (int k = 0; k < (G::HW + TPP - 1) / TPP; ++k) {
+            const int px = lane + k * TPP;
+            if (G::HW % TPP == 0 || px < G::HW) {
+                const int r = px / G::W, c = px - r * G::W;
+                acc += srcq[r * wsi + c];
+            }
+        }
+#pragma unroll
+        for (int m = TPP / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+        if (lane == 0) {
+            const VarSrc<T> vs = vs_of(q);
+            T v[1] = {fma_t(w, acc, b)};
+            const int at[1] = {q * arena};
+            const bool ok[1] = {true};
+            T u1[1] = {T(1)}, u2[1] = {T(1)};
             if (vs.on) {
                 u1[0] = vs.x[0];
                 u2[0] = vs.y[0];
@@ -322,32 +386,38 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::POINT) {
-        constexpr int KP = (G::HOWO + kNT - 1) / kNT;
+        constexpr int N = NP * G::HOWO;
+        constexpr int KP = (N + kNT - 1) / kNT;
         T u1[KP], u2[KP], v[KP];
         int at[KP];
         bool ok[KP];
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
-            const int px = tid + k * kNT;
-            ok[k] = G::HOWO % kNT == 0 || px < G::HOWO;
-            const int pc = ok[k] ? px : 0;
+            const int e = tid + k * kNT;
+            ok[k] = N % kNT == 0 || e < N;
+            const int ec = ok[k] ? e : 0;
+            const int q = NP == 1 ? 0 : ec / G::HOWO, pc = ec - q * G::HOWO;
             const int r = pc / G::WO, c = pc - r * G::WO;
-            at[k] = r * wso + c;
+            const VarSrc<T> vs = vs_of(q);
+            at[k] = q * arena + r * wso + c;
             u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
             u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
-            v[k] = fma_t(w, src[(r * G::S) * wsi + c * G::S], b);
+            v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
         net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
     } else {
         T* __restrict__ hs = lds + p.hs;
+        constexpr int NHT = NP * G::NH, NVT = NP * G::NV, NZT = NP * G::NZ;
         // variances of this thread's outputs, in flight during the row pass
         T u1[G::KV][G::R3], u2[G::KV][G::R3];
-        if (vs.on) {
+        if (vs0.on) {
 #pragma unroll
             for (int kv = 0; kv < G::KV; ++kv) {
                 const int it = tid + kv * kNT;
-                const int itc = (G::NV % kNT == 0 || it < G::NV) ? it : 0;
-                const int g3 = itc / G::WO, c = itc - g3 * G::WO;
+                const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
+                const int q = NP == 1 ? 0 : itc / G::NV, l = itc - q * G::NV;
+                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const VarSrc<T> vs = vs_of(q);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
                     u1[kv][k] = vs.x[(g3 * G::R3 + k) * G::WO + c];
@@ -364,15 +434,17 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
         for (int kh = 0; kh < G::KH; ++kh) {
             const int it = tid + kh * kNT;
-            if (G::NH % kNT == 0 || it < G::NH) {
-                const int qi = it / G::NG2, g2 = it - qi * G::NG2;
-                const T* row = src + (G::Q0 + qi + G::OFF) * wsi + g2 * G::R2 * G::S + G::OFF;
+            if (NHT % kNT == 0 || it < NHT) {
+                const int q = NP == 1 ? 0 : it / G::NH, l = it - q * G::NH;
+                const int qi = l / G::NG2, g2 = l - qi * G::NG2;
+                const T* row = src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
+                               g2 * G::R2 * G::S + G::OFF;
                 T win[G::WIN2];
 #pragma unroll
                 for (int t = 0; t < G::WIN2; ++t) win[t] = row[t];
                 T o[G::R2];
                 win_sums<T, G::TAPS, G::S, G::R2>(win, o);
-                T* h = hs + (G::Q0 + qi) * G::WO + g2 * G::R2;
+                T* h = hs + q * arena + (G::Q0 + qi) * G::WO + g2 * G::R2;
 #pragma unroll
                 for (int t = 0; t < G::R2; ++t) h[t] = o[t];
             }
@@ -380,10 +452,12 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // hs rows outside the input are zero (the scratch is shared by every conv)
         if constexpr (G::NZ > 0) {
 #pragma unroll
-            for (int z0 = 0; z0 < G::NZ; z0 += kNT) {
+            for (int z0 = 0; z0 < NZT; z0 += kNT) {
                 const int z = z0 + tid;
-                if (G::NZ % kNT == 0 || z < G::NZ)
-                    hs[z < G::Q0 * G::WO ? z : z + G::NVR * G::WO] = T(0);
+                if (NZT % kNT == 0 || z < NZT) {
+                    const int q = NP == 1 ? 0 : z / G::NZ, zl = z - q * G::NZ;
+                    hs[q * arena + (zl < G::Q0 * G::WO ? zl : zl + G::NVR * G::WO)] = T(0);
+                }
             }
         }
         lds_barrier();
@@ -392,9 +466,10 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
-            if (G::NV % kNT == 0 || it < G::NV) {
-                const int g3 = it / G::WO, c = it - g3 * G::WO;
-                const T* col = hs + g3 * G::R3 * G::S * G::WO + c;
+            if (NVT % kNT == 0 || it < NVT) {
+                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
+                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const T* col = hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
@@ -405,7 +480,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
                     v[k] = fma_t(w, o[k], b);
-                    at[k] = (g3 * G::R3 + k) * wso + c;
+                    at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
                 net_out<T, EX, DU, G::R3>(lds, op, v, at, ok, u1[kv], u2[kv], tab);
@@ -415,33 +490,46 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 }
 
 // ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
-// One pass: KE pixels per thread at px = base + k·kNT + tid.
-template <typename T, bool EX, bool DU, int KIND, int KE, int W_>
+// One pass: KE pixels per thread at e = base + k·kNT + tid over the NP pairs' maps
+// (pair q = e / hw; NP > 1 needs the compile-time size W_).
+template <typename T, bool EX, bool DU, int KIND, int KE, int W_, int NP>
 __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op& op,
-                                          const NetP<T>& p, unsigned i, unsigned j, int tid,
+                                          const NetP<T>& p, const Pairs& pr, int tid,
                                           int base, int hw, const PolyTab& tab) {
+    static_assert(NP == 1 || W_ > 0, "multi-pair elementwise ops need a compile-time size");
     const int wd = W_ ? W_ : op.w, ws = op.ws_out;
+    const int arena = NP == 1 ? 0 : p.lds_elems;
     const FastDiv fw{op.div_m, op.div_s, (unsigned)op.w};
     // RELU reads (var_x, var_y) = variances of src (an elementwise ReLU has no dst2);
     // LINEAR may carry a dst2 ReLU with (var2_x, var2_y)
-    const VarSrc<T> vs = KIND == CGP_NET_RELU
-                             ? VarSrc<T>{gptr<T>(op.var_x) + (size_t)i * hw,
-                                         gptr<T>(op.var_y) + (size_t)j * hw, true}
-                             : var_src<T>(op, i, j, hw);
-    const GP<T> xi = gptr<T>(p.x) + (size_t)i * p.channels * hw;
-    const GP<T> yj = gptr<T>(p.y) + (size_t)j * p.channels * hw;
+    auto vs_of = [&](unsigned iq, unsigned jq) {
+        return KIND == CGP_NET_RELU ? VarSrc<T>{gptr<T>(op.var_x) + (size_t)iq * hw,
+                                                gptr<T>(op.var_y) + (size_t)jq * hw, true}
+                                    : var_src<T>(op, iq, jq, hw);
+    };
+    const VarSrc<T> vs0 = vs_of(pr.i, pr.j);
+    const GP<T> xi = gptr<T>(p.x) + (size_t)pr.i * p.channels * hw;
+    const GP<T> yj = gptr<T>(p.y) + (size_t)pr.j * p.channels * hw;
+    const int n = NP * hw;
     // waves with no pixel in this pass skip the ReLUs (uniform per wave)
-    const bool live = base + (tid & ~63) < hw;
+    const bool live = base + (tid & ~63) < n;
     T a[KE], u1[KE], u2[KE];
     int at[KE];
     bool ok[KE];
 #pragma unroll
     for (int k = 0; k < KE; ++k) {
-        const int px = base + k * kNT + tid;
-        ok[k] = px < hw;
-        const int pc = ok[k] ? px : 0;
+        const int e = base + k * kNT + tid;
+        ok[k] = e < n;
+        const int ec = ok[k] ? e : 0;
+        const int q = NP == 1 ? 0 : ec / hw, pc = ec - q * hw;
         const int r = W_ ? pc / W_ : (int)fdiv((unsigned)pc, fw);
-        at[k] = r * ws + (pc - r * wd);
+        at[k] = q * arena + r * ws + (pc - r * wd);
+        VarSrc<T> vs = vs0;
+        if constexpr (NP > 1) {
+            unsigned iq, jq;
+            pair_q<NP>(pr, q, iq, jq);
+            vs = vs_of(iq, jq);
+        }
         u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
         u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
         if constexpr (KIND == CGP_NET_RELU) {
@@ -478,30 +566,53 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
 
 // compile-time map size: passes of at most kEw pixels per thread, the last one sized to
 // what is left (28x28: 4 + 3)
-template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int P>
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP, int PI>
 __device__ __forceinline__ void elem_passes(T* __restrict__ lds, const cgp_net_op& op,
-                                            const NetP<T>& p, unsigned i, unsigned j,
-                                            int tid, const PolyTab& tab) {
-    constexpr int KF = (H_ * W_ + kNT - 1) / kNT;
-    if constexpr (P * kEw < KF) {
-        constexpr int KE = KF - P * kEw < kEw ? KF - P * kEw : kEw;
-        elem_pass<T, EX, DU, KIND, KE, W_>(lds, op, p, i, j, tid, P * kEw * kNT, H_ * W_, tab);
-        elem_passes<T, EX, DU, KIND, H_, W_, P + 1>(lds, op, p, i, j, tid, tab);
+                                            const NetP<T>& p, const Pairs& pr, int tid,
+                                            const PolyTab& tab) {
+    constexpr int KF = (NP * H_ * W_ + kNT - 1) / kNT;
+    if constexpr (PI * kEw < KF) {
+        constexpr int KE = KF - PI * kEw < kEw ? KF - PI * kEw : kEw;
+        elem_pass<T, EX, DU, KIND, KE, W_, NP>(lds, op, p, pr, tid, PI * kEw * kNT, H_ * W_,
+                                               tab);
+        elem_passes<T, EX, DU, KIND, H_, W_, NP, PI + 1>(lds, op, p, pr, tid, tab);
     }
 }
 
-// H_ = W_ = 0: runtime map size (generic path).
-template <typename T, bool EX, bool DU, int KIND, int H_, int W_>
+// H_ = W_ = 0: runtime map size (generic path, one pair per workgroup).
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP>
 __device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
-                                         const NetP<T>& p, unsigned i, unsigned j) {
+                                         const NetP<T>& p, const Pairs& pr) {
     const int tid = opaque_tid();
     const PolyTab tab = poly_table();
     if constexpr (H_ == 0) {
         const int hw = op.h * op.w;
         for (int base = 0; base < hw; base += kEw * kNT)
-            elem_pass<T, EX, DU, KIND, kEw, 0>(lds, op, p, i, j, tid, base, hw, tab);
+            elem_pass<T, EX, DU, KIND, kEw, 0, 1>(lds, op, p, pr, tid, base, hw, tab);
     } else {
-        elem_passes<T, EX, DU, KIND, H_, W_, 0>(lds, op, p, i, j, tid, tab);
+        elem_passes<T, EX, DU, KIND, H_, W_, NP, 0>(lds, op, p, pr, tid, tab);
+    }
+}
+
+// Stage boundary (CGP_NET_LOAD / CGP_NET_STORE): the map of each of the NP pairs moves
+// between its slot and the unit's state record, state[(u - ubeg) · code + add + pixel].
+template <typename T, int KIND, int NP>
+__device__ __forceinline__ void net_move(T* __restrict__ lds, const cgp_net_op& op,
+                                         const NetP<T>& p, const Pairs& pr) {
+    const int tid = opaque_tid();
+    const int hw = op.h * op.w, n = NP * hw;
+    const int arena = NP == 1 ? 0 : p.lds_elems;
+    T* state = const_cast<T*>(static_cast<const T*>(op.var_x));
+    for (int e = tid; e < n; e += kNT) {
+        const int q = NP == 1 ? 0 : e / hw, l = e - q * hw;
+        const int r = l / op.w, c = l - r * op.w;
+        // the state buffer holds the units of this launch, [ubeg, uend)
+        const size_t g = (size_t)(pr.u0 + q - p.ubeg) * (size_t)op.code + (size_t)op.add +
+                         (size_t)l;
+        if constexpr (KIND == CGP_NET_LOAD)
+            lds[op.dst + q * arena + r * op.ws_out + c] = state[g];
+        else
+            state[g] = lds[op.src + q * arena + r * op.ws_in + c];
     }
 }
 
@@ -539,6 +650,23 @@ __device__ __forceinline__ void tri_decode(unsigned s, unsigned nb, unsigned& bi
     bj = (unsigned)(r + ((long long)s - off(r)));
 }
 
+// tile unit u (supertile, pair within it) -> (i, j); false if outside the tile
+template <typename T>
+__device__ __forceinline__ bool unit_pair(const NetP<T>& p, long long u, unsigned& i,
+                                          unsigned& j) {
+    const unsigned s = (unsigned)(u >> (2 * kSTL)), q = (unsigned)u & (kST * kST - 1u);
+    unsigned bi, bj;
+    if (p.same) {
+        tri_decode(s, p.nbi, bi, bj);
+    } else {
+        bi = s / p.nbj;
+        bj = s - bi * p.nbj;
+    }
+    i = bi * kST + (q >> kSTL);
+    j = bj * kST + (q & (kST - 1u));
+    return u < p.units && i < p.n1 && j < p.n2;
+}
+
 constexpr int geo_index(int h, int w, int ho, int wo, int k, int s, int o) {
     for (int n = 0; n < kNumGeo; ++n) {
         const GeoRow& g = kGeoTable[n];
@@ -549,99 +677,146 @@ constexpr int geo_index(int h, int w, int ho, int wo, int k, int s, int o) {
     return -1;
 }
 
+// a geometry / map size is instantiated for NP pairs when the NP maps fit the passes
+// (NP·h·w <= 1024: 4 pairs at <= 16x16, 16 at <= 8x8); the host stages networks to match
+#define CGP_NET_FITS(h, w) (NP == 1 || (h) * (w) * NP <= 1024)
+
 #define CGP_NET_CASE(h, w, ho, wo, k, s, o)                                          \
     case geo_index(h, w, ho, wo, k, s, o):                                           \
-        net_conv<T, EX, DU, NG<h, w, ho, wo, k, s, o>>(lds, op, p, i, j);                    \
+        if constexpr (CGP_NET_FITS(h, w))                                            \
+            net_conv<T, EX, DU, NG<h, w, ho, wo, k, s, o, NP>>(lds, op, p, pr);      \
         break;
 
 #define CGP_NET_RES_CASE(h, w)                                                        \
     case res_index(h, w):                                                             \
-        net_elem<T, EX, DU, KIND, h, w>(lds, op, p, i, j);                                \
+        if constexpr (CGP_NET_FITS(h, w)) net_elem<T, EX, DU, KIND, h, w, NP>(lds, op, p, pr); \
         break;
 
 // only the ReLU is worth a per-size instantiation (MOMENTS runs once per pair, LINEAR
-// only for Mixture / multi-term Sum); fewer cases also keep the SGPR budget
-template <typename T, bool EX, bool DU, int KIND>
+// only for Mixture / multi-term Sum); fewer cases also keep the SGPR budget.  Multi-pair
+// stages run compile-time sizes only (the host keeps moments and other sizes at NP = 1).
+template <typename T, bool EX, bool DU, int KIND, int NP>
 __device__ __forceinline__ void net_elem_dispatch(T* __restrict__ lds, const cgp_net_op& op,
-                                                  const NetP<T>& p, unsigned i, unsigned j) {
-    if constexpr (KIND == CGP_NET_RELU) {
+                                                  const NetP<T>& p, const Pairs& pr) {
+    if constexpr (KIND == CGP_NET_RELU || (KIND == CGP_NET_LINEAR && NP > 1)) {
         switch (op.code) {
             CGP_NET_RESOLUTIONS(CGP_NET_RES_CASE)
         default:
-            net_elem<T, EX, DU, KIND, 0, 0>(lds, op, p, i, j);
+            if constexpr (NP == 1) net_elem<T, EX, DU, KIND, 0, 0, 1>(lds, op, p, pr);
             break;
         }
-    } else {
-        net_elem<T, EX, DU, KIND, 0, 0>(lds, op, p, i, j);
+    } else if constexpr (NP == 1) {
+        net_elem<T, EX, DU, KIND, 0, 0, 1>(lds, op, p, pr);
+    }
+}
+
+template <typename T, bool EX, bool DU, int NP>
+__device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op,
+                                       const NetP<T>& p, const Pairs& pr, int tid) {
+    if (op.zero_halo) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const int qa = NP == 1 ? 0 : q * p.lds_elems;
+            zero_halos(lds + qa, op.dst, op.zero_halo & 0xffff, op.h, op.w, op.ws_out, tid);
+            zero_halos(lds + qa, op.dst2, (unsigned)op.zero_halo >> 16, op.h, op.w,
+                       op.ws_out, tid);
+        }
+    }
+    switch (op.kind) {
+    case CGP_NET_CONV:
+        switch (op.code) {
+            CGP_NET_GEOMETRIES(CGP_NET_CASE)
+        default:
+            break;
+        }
+        break;
+    case CGP_NET_RELU:
+        net_elem_dispatch<T, EX, DU, CGP_NET_RELU, NP>(lds, op, p, pr);
+        break;
+    case CGP_NET_MOMENTS:
+        net_elem_dispatch<T, EX, DU, CGP_NET_MOMENTS, NP>(lds, op, p, pr);
+        break;
+    case CGP_NET_LINEAR:
+        net_elem_dispatch<T, EX, DU, CGP_NET_LINEAR, NP>(lds, op, p, pr);
+        break;
+    case CGP_NET_LOAD:
+        net_move<T, CGP_NET_LOAD, NP>(lds, op, p, pr);
+        break;
+    case CGP_NET_STORE:
+        net_move<T, CGP_NET_STORE, NP>(lds, op, p, pr);
+        break;
+    default:
+        break;
     }
 }
 
 // WPE: waves per SIMD the register allocation targets (amdgpu_waves_per_eu).  LDS caps
 // the resident workgroups per CU (two waves each) at 160 KB / footprint, so allocating
 // registers for more waves than that only forces spills; net_launch picks WPE from the
-// LDS footprint (net_wpe).
-template <typename T, bool EX, bool DU, int WPE>
+// LDS footprint (net_wpe).  NP: pairs per workgroup (1, or 4 / 16 for small-map stages).
+template <typename T, bool EX, bool DU, int WPE, int NP>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
+    __shared__ unsigned pair_tab[2 * kMaxNP];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
-    for (int e = tid; e < p.lds_elems; e += kNT) lds[e] = T(0);   // slot halos stay zero
+    for (int e = tid; e < NP * p.lds_elems; e += kNT) lds[e] = T(0);   // slot halos stay zero
     lds_barrier();
     // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
-    // contiguous run of supertiles and its L2 holds the images/variances they share
+    // contiguous run of supertiles and its L2 holds the images/variances they share.
+    // Ranges and groups are whole multiples of NP units.
     const unsigned g8 = gridDim.x / 8, xcd = blockIdx.x % 8, l = blockIdx.x / 8;
-    const long long per = (p.units + 7) / 8;
-    const long long beg = (long long)xcd * per;
-    const long long end = beg + per < p.units ? beg + per : p.units;
-    for (long long u = beg + l; u < end; u += g8) {
-        const unsigned s = (unsigned)(u >> (2 * kSTL)), q = (unsigned)u & (kST * kST - 1u);
-        unsigned bi, bj;
-        if (p.same) {
-            tri_decode(s, p.nbi, bi, bj);
+    const long long span = p.uend - p.ubeg;
+    const long long per = ((span + 7) / 8 + NP - 1) / NP * NP;
+    const long long beg = p.ubeg + (long long)xcd * per;
+    const long long end = beg + per < p.uend ? beg + per : p.uend;
+    for (long long u = beg + (long long)l * NP; u < end; u += (long long)g8 * NP) {
+        Pairs pr;
+        pr.tab = pair_tab;
+        pr.u0 = u;
+        if constexpr (NP == 1) {
+            if (!unit_pair(p, u, pr.i, pr.j)) continue;
+            if (p.same && pr.j <= pr.i) {
+                if (p.final_stage && pr.j == pr.i && tid == 0)
+                    p.out[(long long)pr.i * p.ldo + pr.i] = p.kdiag[pr.i];
+                continue;
+            }
         } else {
-            bi = s / p.nbj;
-            bj = s - bi * p.nbj;
-        }
-        const unsigned i = bi * kST + (q >> kSTL), j = bj * kST + (q & (kST - 1u));
-        if (i >= p.n1 || j >= p.n2) continue;
-        if (p.same && j <= i) {
-            if (j == i && tid == 0) p.out[(long long)i * p.ldo + i] = p.kdiag[i];
-            continue;
+            // the group's pair table; pairs outside the tile are computed on clamped
+            // indices and never stored
+            if (tid < NP) {
+                unsigned iq = 0, jq = 0;
+                unit_pair(p, u + tid, iq, jq);
+                pair_tab[tid] = iq < p.n1 ? iq : p.n1 - 1;
+                pair_tab[kMaxNP + tid] = jq < p.n2 ? jq : p.n2 - 1;
+            }
+            pr.i = pr.j = 0;
+            lds_barrier();
         }
         for (int k = 0; k < p.nops; ++k) {
             const cgp_net_op op = p.ops[k];
-            if (op.zero_halo) {
-                zero_halos(lds, op.dst, op.zero_halo & 0xffff, op.h, op.w, op.ws_out, tid);
-                zero_halos(lds, op.dst2, (unsigned)op.zero_halo >> 16, op.h, op.w, op.ws_out,
-                           tid);
-            }
-            switch (op.kind) {
-            case CGP_NET_CONV:
-                switch (op.code) {
-                    CGP_NET_GEOMETRIES(CGP_NET_CASE)
-                default:
-                    break;
-                }
-                break;
-            case CGP_NET_RELU:
-                net_elem_dispatch<T, EX, DU, CGP_NET_RELU>(lds, op, p, i, j);
-                break;
-            case CGP_NET_MOMENTS:
-                net_elem_dispatch<T, EX, DU, CGP_NET_MOMENTS>(lds, op, p, i, j);
-                break;
-            case CGP_NET_LINEAR:
-                net_elem_dispatch<T, EX, DU, CGP_NET_LINEAR>(lds, op, p, i, j);
-                break;
-
-            default:
-                break;
-            }
+            net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
             lds_barrier();
         }
-        if (tid == 0) {
-            const T v = lds[p.final_slot];
-            p.out[(long long)i * p.ldo + j] = v;
-            if (p.same) p.out[(long long)j * p.ldo + i] = v;
+        if (p.final_stage) {
+            if constexpr (NP == 1) {
+                if (tid == 0) {
+                    const T v = lds[p.final_slot];
+                    p.out[(long long)pr.i * p.ldo + pr.j] = v;
+                    if (p.same) p.out[(long long)pr.j * p.ldo + pr.i] = v;
+                }
+            } else if (tid < NP) {
+                unsigned iq, jq;
+                if (u + tid < end && unit_pair(p, u + tid, iq, jq)) {
+                    if (!p.same || jq > iq) {
+                        const T v = lds[tid * p.lds_elems + p.final_slot];
+                        p.out[(long long)iq * p.ldo + jq] = v;
+                        if (p.same) p.out[(long long)jq * p.ldo + iq] = v;
+                    } else if (jq == iq) {
+                        p.out[(long long)iq * p.ldo + iq] = p.kdiag[iq];
+                    }
+                }
+            }
         }
         lds_barrier();
     }
@@ -655,24 +830,38 @@ inline int net_wpe(long long lds_bytes) {
     return w < 3 ? 3 : (w > 5 ? 5 : (int)w);
 }
 
-// the instantiation for (EX, DU, LDS footprint): fp64 closed form — the production path
-// — has a register target per occupancy level; the exact ReLU and fp32 one each
+// the instantiation for (EX, DU, pairs, LDS footprint of the workgroup): the fp64 closed
+// form — the production path — has a register target per occupancy level and the
+// multi-pair stages; the exact ReLU and fp32 run one pair per workgroup
+template <typename T, int NP>
+const void* net_fn_np(bool du, long long lds_bytes) {
+    switch (net_wpe(lds_bytes)) {
+    case 3: return du ? (const void*)net_kernel<T, false, true, 3, NP>
+                      : (const void*)net_kernel<T, false, false, 3, NP>;
+    case 4: return du ? (const void*)net_kernel<T, false, true, 4, NP>
+                      : (const void*)net_kernel<T, false, false, 4, NP>;
+    default: return du ? (const void*)net_kernel<T, false, true, 5, NP>
+                       : (const void*)net_kernel<T, false, false, 5, NP>;
+    }
+}
 template <typename T>
-const void* net_fn(bool ex, bool du, long long lds_bytes) {
-    if (ex) return du ? (const void*)net_kernel<T, true, true, 3>
-                      : (const void*)net_kernel<T, true, false, 3>;
+const void* net_fn(bool ex, bool du, int np, long long lds_bytes) {
+    if (ex) {
+        if (np != 1) return nullptr;
+        return du ? (const void*)net_kernel<T, true, true, 3, 1>
+                  : (const void*)net_kernel<T, true, false, 3, 1>;
+    }
     if constexpr (sizeof(T) == 8) {
-        switch (net_wpe(lds_bytes)) {
-        case 3: return du ? (const void*)net_kernel<T, false, true, 3>
-                          : (const void*)net_kernel<T, false, false, 3>;
-        case 4: return du ? (const void*)net_kernel<T, false, true, 4>
-                          : (const void*)net_kernel<T, false, false, 4>;
-        default: return du ? (const void*)net_kernel<T, false, true, 5>
-                           : (const void*)net_kernel<T, false, false, 5>;
+        switch (np) {
+        case 1: return net_fn_np<T, 1>(du, lds_bytes);
+        case 4: return net_fn_np<T, 4>(du, lds_bytes);
+        case 16: return net_fn_np<T, 16>(du, lds_bytes);
+        default: return nullptr;
         }
     }
-    return du ? (const void*)net_kernel<T, false, true, 4>
-              : (const void*)net_kernel<T, false, false, 5>;
+    if (np != 1) return nullptr;
+    return du ? (const void*)net_kernel<T, false, true, 4, 1>
+              : (const void*)net_kernel<T, false, false, 5, 1>;
 }
 
 int net_occupancy(const void* fn, int lds_bytes) {
@@ -691,24 +880,27 @@ int net_occupancy(const void* fn, int lds_bytes) {
 }
 
 template <typename T>
-int net_occupancy_for(int lds_bytes, int flags) {
-    return net_occupancy(net_fn<T>(flags & CGP_FLAG_EXACT_RELU, flags & CGP_FLAG_NET_DUAL,
-                                   lds_bytes),
-                         lds_bytes);
+int net_occupancy_for(int lds_bytes, int flags, int np) {
+    const void* fn = net_fn<T>(flags & CGP_FLAG_EXACT_RELU, flags & CGP_FLAG_NET_DUAL, np,
+                               (long long)lds_bytes * np);
+    return fn ? net_occupancy(fn, lds_bytes * np) : 0;
 }
 
 template <typename T>
-int net_launch(const NetP<T>& p, bool ex, bool du, long long lds_bytes, void* stream) {
-    const void* fn = net_fn<T>(ex, du, lds_bytes);
-    const int per_cu = net_occupancy(fn, (int)lds_bytes);
+int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, void* stream) {
+    const long long wg_bytes = lds_bytes * np;
+    const void* fn = net_fn<T>(ex, du, np, wg_bytes);
+    if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
+    const int per_cu = net_occupancy(fn, (int)wg_bytes);
     if (per_cu <= 0)
-        return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", lds_bytes);
+        return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", wg_bytes);
+    const long long groups = (p.uend - p.ubeg + np - 1) / np;
     long long grid = (long long)per_cu * device_cus();
-    if (grid > p.units) grid = p.units;
+    if (grid > groups) grid = groups;
     grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
     NetP<T> arg = p;
     void* args[] = {&arg};
-    CGP_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args, (size_t)lds_bytes,
+    CGP_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args, (size_t)wg_bytes,
                             as_stream(stream)));
     return check_launch("net_kernel");
 }
@@ -755,8 +947,24 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.hs = a->hs;
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
+    const int np = a->pairs <= 0 ? 1 : a->pairs;
+    if (np != 1 && np != 4 && np != kMaxNP)
+        return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 4 or 16)", np);
+    if (lds_bytes * np > 160 * 1024)
+        return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * np);
+    if (a->unit_begin == 0 && a->unit_end == 0) {
+        p.ubeg = 0;
+        p.uend = p.units;
+    } else {
+        p.ubeg = a->unit_begin;
+        p.uend = a->unit_end;
+    }
+    if (p.ubeg < 0 || p.uend > p.units || p.ubeg >= p.uend || p.ubeg % np)
+        return fail(CGP_EINVAL, "net: unit range [%lld, %lld) of %lld", (long long)p.ubeg,
+                    (long long)p.uend, (long long)p.units);
+    p.final_stage = a->final_stage;
     const bool du = (a->flags & CGP_FLAG_NET_DUAL) != 0;
-    return net_launch<T>(p, p.exact != 0, du, lds_bytes, stream);
+    return net_launch<T>(p, p.exact != 0, du, np, lds_bytes, stream);
 }
 
 }  // namespace
@@ -783,10 +991,11 @@ int cgp_net_hs_elems(int32_t code) {
     return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;
 }
 
-int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags) {
-    if (lds_bytes <= 0 || lds_bytes > 160 * 1024) return 0;
-    return f64 ? net_occupancy_for<double>(lds_bytes, flags)
-               : net_occupancy_for<float>(lds_bytes, flags);
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs) {
+    if (pairs <= 0) pairs = 1;
+    if (lds_bytes <= 0 || (long long)lds_bytes * pairs > 160 * 1024) return 0;
+    return f64 ? net_occupancy_for<double>(lds_bytes, flags, pairs)
+               : net_occupancy_for<float>(lds_bytes, flags, pairs);
 }
 
 int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }

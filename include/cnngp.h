@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 3
+#define CGP_ABI_VERSION 4
 
 /* error codes */
 #define CGP_OK 0
@@ -205,6 +205,15 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
  *   CGP_NET_CONV     dst = w·Σ_window src + b  [→ ReLU] [+ add]    kernels.py:92-98
  *   CGP_NET_RELU     dst = relu(src)           [+ add]            kernels.py:134-165
  *   CGP_NET_LINEAR   dst = weight·src + bias·add   (Sum / Mixture: kernels.py:220-254)
+ *   CGP_NET_LOAD / CGP_NET_STORE   move a map between a slot and the per-unit state
+ *                    record (var_x = the state buffer of the launch's units: record of
+ *                    unit u at (u - unit_begin)·code elements; add = the map's offset in
+ *                    the record) at a stage boundary
+ *
+ * Stages.  A network whose tail runs on small maps (a ResNet's 14x14 and 7x7 blocks)
+ * is split at the resolution drops: the tail stages run several pairs per workgroup
+ * (`pairs` = 4 at <= 16x16, 16 at <= 8x8), so a small map's ops still fill the
+ * workgroup; the live maps cross a boundary through the state buffer.
  *
  * Same tiles (same=1) evaluate only i < j, mirror K[j, i] = K[i, j] (the recursion is
  * symmetric in (i, j) when y = x) and take K[i, i] = kdiag[i] — the per-image
@@ -215,6 +224,8 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
 #define CGP_NET_RELU 1
 #define CGP_NET_MOMENTS 2
 #define CGP_NET_LINEAR 3
+#define CGP_NET_LOAD 4     /* stage input:  slot dst <- state[unit][add .. add + h·w) */
+#define CGP_NET_STORE 5    /* stage output: state[unit][add .. add + h·w) <- slot src */
 
 typedef struct cgp_net_op {
     int32_t kind;          /* CGP_NET_* */
@@ -250,9 +261,14 @@ typedef struct cgp_net_args {
     int32_t same;          /* 1: y is x (Kxx diagonal tile) */
     int32_t final_slot;    /* LDS offset of the 1x1 result */
     int32_t hs;            /* LDS offset of the row-sum scratch */
-    int32_t lds_elems;     /* LDS footprint (elements of the compute type) */
+    int32_t lds_elems;     /* LDS footprint of ONE pair (elements of the compute type) */
     int32_t flags;         /* CGP_FLAG_EXACT_RELU */
-    int32_t reserved;
+    int32_t pairs;         /* pairs per workgroup: 1, or 4 / 16 for a stage whose maps are
+                              at most 16x16 / 8x8 (each pair gets its own lds_elems arena) */
+    int64_t unit_begin;    /* the tile's pair units this launch covers, [begin, end): unit */
+    int64_t unit_end;      /* u = 64·supertile + 8·(i % 8) + j % 8; 0, 0 = the whole tile */
+    int32_t final_stage;   /* 1: write K (the last stage); 0: the ops end in CGP_NET_STORE */
+    int32_t reserved2;
 } cgp_net_args;
 
 /* Geometry code of a conv for CGP_NET_CONV, or -1 if the fused kernel has no
@@ -268,8 +284,9 @@ int cgp_net_resolution(int32_t h, int32_t w);
 /* cgp_net_args.flags: CGP_FLAG_EXACT_RELU, and CGP_FLAG_NET_DUAL when any op has dst2
  * (selects the kernel instantiation with the dual output stage) */
 #define CGP_FLAG_NET_DUAL 4
-/* workgroups per CU the fused kernel reaches with lds_bytes of LDS (0 if it cannot run) */
-int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags);
+/* workgroups per CU the fused kernel reaches with lds_bytes of LDS per pair and `pairs`
+ * pairs per workgroup (0 if it cannot run) */
+int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs);
 int cgp_net_f64(const cgp_net_args* args, void* stream);
 int cgp_net_f32(const cgp_net_args* args, void* stream);
 

@@ -65,19 +65,18 @@ def _relu(c, v1, v2):
         return (sin + (math.pi - np.arccos(cos)) * c) / (2 * math.pi)
 
 
-def run_pair(net, x_i, y_j, var, i, j, lds=None):
-    """One pair through the op list.  ``lds`` persists across the pairs of a workgroup
-    (the kernel zeroes it once per workgroup), so stale values of earlier pairs stay in
-    every cell an op does not write — as on the device."""
-    if lds is None:
-        lds = np.zeros(net.lds_elems)
-    hs0 = net.hs
+def run_stage(stage, x_i, y_j, var, i, j, lds, state):
+    """One pair through one stage's op list.  ``lds`` (this pair's arena) persists
+    across the pairs a workgroup walks (the kernel zeroes it once per workgroup), so
+    stale values of earlier pairs stay in every cell an op does not write — as on the
+    device.  ``state``: {"in": record, "out": record} of this pair's unit."""
+    hs0 = 0
 
     def plane(off, h, w, ws):
         idx = off + np.arange(h)[:, None] * ws + np.arange(w)[None, :]
         return idx
 
-    for f, v in net.records:
+    for f, v in stage.records:
         kind = f["kind"]
         for key, dst in (("zero", f["dst"]), ("zero2", f.get("dst2", -1))):
             if key in f:                                        # cgp_net_op.zero_halo
@@ -86,7 +85,15 @@ def run_pair(net, x_i, y_j, var, i, j, lds=None):
                 for r in range(f["h"]):
                     c0 = dst + r * f["ws_out"] + f["w"]
                     lds[c0:c0 + gap] = 0.0
-        if kind == 2:                                           # MOMENTS
+        if kind == 4:                                           # LOAD
+            h, w = f["h"], f["w"]
+            lds[plane(f["dst"], h, w, f["ws_out"])] = \
+                state["in"][f["add"]:f["add"] + h * w].reshape(h, w)
+        elif kind == 5:                                         # STORE
+            h, w = f["h"], f["w"]
+            state["out"][f["add"]:f["add"] + h * w] = \
+                lds[plane(f["src"], h, w, f["ws_in"])].reshape(-1)
+        elif kind == 2:                                         # MOMENTS
             h, w = f["h"], f["w"]
             C = x_i.shape[0]
             lds[plane(f["dst"], h, w, f["ws_out"])] = (x_i * y_j).sum(0) / C
@@ -132,14 +139,17 @@ def run_pair(net, x_i, y_j, var, i, j, lds=None):
             if f.get("dst2", -1) >= 0:
                 vx, vy = var[f["var2"]]
                 lds[plane(f["dst2"], h, w, f["ws_out"])] = _relu(out, vx[i], vy[j])
-    return lds[net.final_slot]
+    return lds[stage.final_slot]
 
 
 def kernel(net, x, y, same):
+    """K through every stage.  One workgroup walks all pairs; a stage with P pairs per
+    workgroup gives pair n the arena n % P (each arena keeps its stale cells)."""
     var = variances(net.plan, x, y)
     n1, n2 = x.shape[0], y.shape[0]
     K = np.zeros((n1, n2))
-    lds = np.zeros(net.lds_elems)           # one workgroup walks every pair
+    arenas = [[np.zeros(st.lds_elems) for _ in range(st.pairs)] for st in net.stages]
+    n = 0
     for i in range(n1):
         for j in range(n2):
             if same and i == j:
@@ -147,5 +157,11 @@ def kernel(net, x, y, same):
             elif same and j < i:
                 K[i, j] = K[j, i]
             else:
-                K[i, j] = run_pair(net, x[i], y[j], var, i, j, lds)
+                rec = None
+                for s, st in enumerate(net.stages):
+                    state = {"in": rec, "out": np.zeros(st.store_stride)}
+                    v = run_stage(st, x[i], y[j], var, i, j, arenas[s][n % st.pairs], state)
+                    rec = state["out"]
+                K[i, j] = v
+                n += 1
     return K

@@ -348,6 +348,43 @@ def test_netfuse_ragged_tiles_vs_oracle(n1, n2):
     assert rel_err(gxx, O.kernel(spec, Z)) < RTOL64["fast"]
 
 
+@pytest.mark.parametrize("cfg", ["mnist_as_tf", "cifar10"])
+@pytest.mark.parametrize("same", [False, True])
+def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, monkeypatch):
+    """multi-pair stages (4 / 16 pairs per workgroup on the 14x14 / 7x7 tail) against the
+    one-stage program and the oracle, with the state buffers chunked to 64 units per
+    launch group so every launch carries a unit range and a range-relative state index"""
+    from cnn_gp import netplan
+    from cnn_gp.program import Plan
+    monkeypatch.setattr(netplan, "CHUNK_BYTES", 64 * 8 * 512)
+    C, side = specs.GEOMETRY[cfg]
+    rng = np.random.default_rng(31)
+    X = rng.random((21, C, side, side))
+    Z = X if same else rng.random((19, C, side, side))
+    m = configs_util.model(cfg).double().to(DEV)
+    plan = m._plan(side, side)
+    multi = netplan.NetPlan(plan, 8)
+    single = netplan.NetPlan(plan, 8, stages=False)
+    assert [st.pairs for st in multi.stages] == [1, 4, 16]
+    assert len(single.stages) == 1
+    x, z = dev(X), dev(Z)
+    n1, n2 = len(X), len(Z)
+    s = stream()
+    var0 = torch.empty((n1 + n2, side, side), dtype=torch.float64, device=DEV)
+    N.check(N.load().cgp_moments_var_f64(N.ptr(x), N.ptr(z), n1, n2, C, side * side,
+                                         N.ptr(var0[:n1]), N.ptr(var0[n1:]), s), "mv")
+    var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, s,
+                             need=multi.need_var | single.need_var)
+    a = multi.run(x, z, var, n1, n2, same, s).cpu().numpy()
+    b = single.run(x, z, var, n1, n2, same, s).cpu().numpy()
+    assert rel_err(a, b) < 1e-12
+    ref = O.kernel(specs.CONFIGS[cfg](), X) if same else \
+        O.kernel(specs.CONFIGS[cfg](), X, Z, False, False)
+    if same:                                   # the kernel fills both triangles
+        assert np.array_equal(a, a.T)
+    assert rel_err(a, ref) < RTOL64["fast"]
+
+
 def test_netfuse_mixture_and_multiterm_sum():
     """LINEAR ops: a 3-branch Mixture and a 3-term Sum at 28x28 (fused geometries)"""
     spec_m = cnn_gp.Sequential(

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--configs", default="mnist_paper_convnet_gp,mnist_paper_residual_cnn_gp,"
                                          "mnist_as_tf,cifar10")
     ap.add_argument("--same", action="store_true", help="Kxx diagonal tile (i<j pairs)")
+    ap.add_argument("--per-stage", action="store_true",
+                    help="also time each stage's launches (multi-pair stages)")
     args = ap.parse_args()
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     B = args.tile
@@ -65,10 +67,38 @@ def main():
         torch.cuda.synchronize()
         ms_fwd = (time.perf_counter() - t0) / args.reps * 1e3
         pairs = B * (B - 1) // 2 if args.same else B * B
-        print(f"{name:30s} ops={net.n_ops:3d} lds={net.lds_elems * X.element_size():6d}B "
-              f"occ={lib.cgp_net_occupancy(net.lds_elems * X.element_size(), int(dt == torch.float64), 4 if net.dual else 0)} "
-              f"net {ms_net:8.2f} ms ({pairs / ms_net / 1e3:7.2f} M pairs/s)  "
-              f"forward {ms_fwd:8.2f} ms")
+        if args.per_stage and len(net.stages) > 1:
+            from cnn_gp import netplan as NP_
+            lib_fn = getattr(lib, f"cgp_net_{sfx}")
+            ev = []
+
+            class Timed:
+                def __call__(self, a, st):
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    rc = lib_fn(a, st)
+                    e1.record(s)
+                    ev.append((a._obj.pairs, e0, e1))
+                    return rc
+            real = N.load
+            N.load = lambda: type("L", (), {f"cgp_net_{sfx}": Timed()})()
+            try:
+                net.run(X, Z, var, B, B, args.same, sh, plan.flags, out=out)
+            finally:
+                N.load = real
+            torch.cuda.synchronize()
+            per = {}
+            for pairs_, e0, e1 in ev:
+                per[pairs_] = per.get(pairs_, 0.0) + e0.elapsed_time(e1)
+            print("   per stage (ms): " + "  ".join(f"{k}p {v:.2f}" for k, v in per.items()))
+        it = X.element_size()
+        stages = " ".join(
+            f"[{st.pairs}p {st.n_ops}ops {st.lds_elems * it * st.pairs}B "
+            f"occ={lib.cgp_net_occupancy(st.lds_elems * it, int(dt == torch.float64), 4 if st.dual else 0, st.pairs)}]"
+            for st in net.stages)
+        print(f"{name:28s} net {ms_net:8.2f} ms ({pairs / ms_net / 1e3:7.2f} M pairs/s)  "
+              f"forward {ms_fwd:8.2f} ms  {stages}")
 
 
 if __name__ == "__main__":

@@ -71,7 +71,7 @@ def main():
             e1.record(s)
             e1.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
-            occ = lib.cgp_net_occupancy(net.lds_elems * 8, 1, 4 if net.dual else 0)
+            occ = lib.cgp_net_occupancy(net.lds_elems * 8, 1, 4 if net.dual else 0, 1)
             if kind == "none":
                 base[side] = ms
                 print(f"{side:3d} {'base':12s} ops={net.n_ops:3d} occ={occ:2d} {ms:8.3f} ms/tile")
