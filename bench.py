@@ -294,7 +294,7 @@ def main():
         # whole-network kernel has no instantiation for): its dominant conv kernel against
         # the HBM roof — the north star's "Conv2d covariance kernel" target
         with torch.no_grad():
-            ops = probe_kernels(model, X[:B], B, B)
+            ops = probe_kernels(model, X[:B], B, B, reps=3)
         by = {}
         for name, ms, b in ops:
             t = by.setdefault(name, [0.0, 0, 0.0, 0])

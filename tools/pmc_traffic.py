@@ -1,9 +1,10 @@
-"""HBM traffic per launch of the whole-network kernel from rocprofv3 FETCH_SIZE /
-WRITE_SIZE passes (separate runs of tools/netbench.py on one config), corrected as
-MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) counts half the bytes of wide reads on
-gfx950, so bytes = 2·FETCH_SIZE·1024 + WRITE_SIZE·1024.
+"""HBM traffic per tile evaluation of the whole-network kernel (all its stage launches)
+from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs of tools/netbench.py
+--reps 1 on one config: 3 tile evaluations), corrected as MI355X_MICROARCH.md §HBM
+prescribes: FETCH_SIZE (KB) counts half the bytes of wide reads on gfx950, so
+bytes = 2·FETCH_SIZE·1024 + WRITE_SIZE·1024.
 
-    python tools/pmc_traffic.py CONFIG TILE DTYPE FETCH_DIR WRITE_DIR [OUT_JSON]
+    python tools/pmc_traffic.py CONFIG TILE DTYPE FETCH_DIR WRITE_DIR [OUT_JSON [EVALS]]
 """
 import csv
 import glob
@@ -11,7 +12,7 @@ import json
 import sys
 
 
-def per_launch(d, counter):
+def per_tile(d, counter, evals):
     vals = []
     for f in glob.glob(d + "/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
@@ -19,17 +20,18 @@ def per_launch(d, counter):
                 vals.append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no net_kernel {counter} rows under {d}")
-    return sum(vals) / len(vals), len(vals)
+    return sum(vals) / evals, len(vals)
 
 
 def main():
     cfg, tile, dtype, fdir, wdir = sys.argv[1:6]
     out = sys.argv[6] if len(sys.argv) > 6 else None
-    fetch, nf = per_launch(fdir, "FETCH_SIZE")
-    write, nw = per_launch(wdir, "WRITE_SIZE")
+    evals = int(sys.argv[7]) if len(sys.argv) > 7 else 3
+    fetch, nf = per_tile(fdir, "FETCH_SIZE", evals)
+    write, nw = per_tile(wdir, "WRITE_SIZE", evals)
     rec = {"tile": int(tile), "dtype": dtype, "fetch_size_kb": fetch, "write_size_kb": write,
            "hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
-           "launches_averaged": [nf, nw],
+           "tile_evaluations": evals, "dispatches": [nf, nw],
            "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)"}
     print(json.dumps({cfg: rec}, indent=1))
     if out:
