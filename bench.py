@@ -180,10 +180,12 @@ def net_roofline(model, x, cfg_name, timing):
             "pairs_per_launch": pairs // len(timing), "alg_flops_per_pair": fl,
             "alg_flops_per_launch": fl * pairs // len(timing),
             "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
+            "stages": [{"pairs_per_workgroup": st.pairs, "ops": st.n_ops} for st in net.stages],
             "note": "fp64 compute roof (VALU = MFMA = 78.6 TF on MI355X); algorithmic "
                     "flops = the reference's direct-stencil conv flops of the pairs the "
-                    "kernel evaluates (same tiles: i < j); traffic: PMC FETCH/WRITE per "
-                    "launch (profiles/r1/net_traffic.json), scaled to this launch size"}
+                    "kernel evaluates (same tiles: i < j); one launch = one tile (all its "
+                    "stage kernels); traffic: PMC FETCH/WRITE per tile "
+                    "(profiles/r1/net_traffic.json), scaled to this launch size"}
 
 
 def cpu_baseline(cfg_name, dtype, pairs):
