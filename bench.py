@@ -8,9 +8,10 @@ this rank evaluated into a device-resident Kxx.
     python bench.py [--gpus N --steps K --warmup W] [--config C --n N --tile B]
 
 Multi-GPU (one process per GPU, torchrun): the Gram tiles of a Kxx whose size grows with
-the world (n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world) are split across ranks with
-the reference's contiguous balanced split (cnn_gp/data.py:11-19) — no data-path
-collective; per-rank work is ~constant ("scaling": "weak").
+the world (n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world) are split across ranks by
+evaluated pairs (balanced_split: a diagonal tile costs half) — no data-path collective;
+per-rank work is ~constant ("scaling": "weak").  cnn_gp.gram keeps the reference's
+contiguous split (cnn_gp/data.py:11-19) for HDF5-compatible worker files.
 
 value = evaluated pairs (Σ over all tiles of B1·B2) per second, whole job.  Also
 reported: unique Kxx entries/s, the single-GPU build+solve wall-clock (rocSOLVER
@@ -69,6 +70,25 @@ def blocks_for_world(n1: int, tile: int, world: int) -> int:
     while nb * (nb + 1) // 2 < target:
         nb += 1
     return nb
+
+
+def balanced_split(all_tiles, B, n, world):
+    """Per-rank tile lists with equal work: the kernel evaluates a diagonal tile's i < j
+    pairs only (half an off-diagonal tile), so the reference's contiguous split by tile
+    count (cnn_gp/data.py:11-19) would leave the ranks holding fewer diagonal tiles
+    behind.  Longest-processing-time greedy on the pairs each tile evaluates, in the
+    reference's tile order within a rank."""
+    def cost(t):
+        same, i, j = t
+        a, b = min(B, n - i * B), min(B, n - j * B)
+        return a * (a - 1) // 2 if same else a * b
+    load = [0] * world
+    parts = [[] for _ in range(world)]
+    for k in sorted(range(len(all_tiles)), key=lambda k: -cost(all_tiles[k])):
+        r = min(range(world), key=lambda r: load[r])
+        load[r] += cost(all_tiles[k])
+        parts[r].append(k)
+    return [[all_tiles[k] for k in sorted(p)] for p in parts]
 
 
 def op_bytes(op, nmaps, n1, n2, C, item):
@@ -213,10 +233,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CGP_BENCH_BACKEND=gloo: rehearse the multi-rank path with several ranks sharing the
+    # GPUs there are (RCCL needs one rank per GPU); the default is nccl (RCCL over xGMI)
+    backend = os.environ.get("CGP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
 
     cfg = importlib.import_module(f"configs.{args.config}")
@@ -229,8 +257,8 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     X = torch.rand((n_total, C, side, side), generator=g, dtype=dtype).to(dev)
 
-    tiles = tile_schedule(n_total, None, B, rank, world)
     all_tiles = tile_schedule(n_total, None, B, 0, 1)
+    tiles = balanced_split(all_tiles, B, n_total, world)[rank]
 
     def tile_pairs(t):
         _, i, j = t
@@ -262,7 +290,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

@@ -246,3 +246,28 @@ def test_print_timings_passthrough(capsys):
     from cnn_gp.data import print_timings
     assert list(print_timings([1, 2, 3], print_interval=0.0)) == [1, 2, 3]
     assert "3/3 it" in capsys.readouterr().out
+
+
+def test_bench_balanced_split_covers_every_tile_once():
+    """bench.py's multi-GPU split: every tile on exactly one rank, per-rank evaluated
+    pairs within one off-diagonal tile of the mean, reference order within a rank"""
+    import importlib.util
+    import os
+    from cnn_gp.data import tile_schedule
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    B = 1024
+    for world in (1, 2, 3, 4, 8):
+        nb = bench.blocks_for_world(4096, B, world)
+        n = nb * B
+        allt = tile_schedule(n, None, B, 0, 1)
+        parts = bench.balanced_split(allt, B, n, world)
+        assert len(parts) == world
+        assert sorted(t for p in parts for t in p) == sorted(allt)
+        for p in parts:
+            assert p == sorted(p, key=allt.index)
+        cost = lambda t: B * (B - 1) // 2 if t[0] else B * B  # noqa: E731
+        loads = [sum(cost(t) for t in p) for p in parts]
+        assert max(loads) - sum(loads) / world <= B * B
