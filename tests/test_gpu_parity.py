@@ -516,3 +516,29 @@ def test_predict_and_cast():
     f32 = rng.random((3, 7, 5)).astype(np.float32)
     out = cnn_gp.load_kern(f32, 1, device=DEV)
     np.testing.assert_array_equal(out.cpu().numpy(), f32[1].astype(np.float64))
+
+
+@pytest.mark.parametrize("cfg", ["mnist_as_tf", "mnist_paper_convnet_gp"])
+def test_large_tile_properties(cfg, monkeypatch):
+    """a 1536-image Kxx (staged program for the ResNet, state chunks of 64 supertiles):
+    symmetric, diagonal = the per-image variance chain, 48 random entries equal to the
+    same pair evaluated alone, positive definite (rocSOLVER Cholesky through solve)"""
+    from cnn_gp import netplan
+    monkeypatch.setattr(netplan, "CHUNK_BYTES", 64 * 64 * 392 * 8)
+    C, side = specs.GEOMETRY[cfg]
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand((1536, C, side, side), generator=g, dtype=torch.float64).to(DEV)
+    m = configs_util.model(cfg).double().to(DEV)
+    with torch.no_grad():
+        K = m(X)
+        assert torch.equal(K, K.T)
+        d = m(X, X, True, True)
+        assert rel_err(torch.diagonal(K).cpu().numpy(), d.cpu().numpy()) < 1e-13
+        rng = np.random.default_rng(6)
+        for a, b in rng.integers(0, 1536, size=(48, 2)):
+            one = m(X[a:a + 1], X[b:b + 1], False, False).item()
+            assert abs(K[a, b].item() - one) <= 1e-12 * abs(one) or a == b
+    Y = torch.ones((1536, 1), dtype=torch.float64, device=DEV)
+    sol = cnn_gp.solve_system(K.clone(), Y)
+    r = (K @ sol - Y).norm() / Y.norm()
+    assert float(r) < 1e-6
