@@ -172,6 +172,23 @@ def alg_flops_per_pair(plan):
     return f
 
 
+def alg_flops_pointwise_per_pair(plan):
+    """The reference's elementwise work per pair on top of the conv stencils: the bias
+    add after every F.conv2d (kernels.py:98), the ReLU map's 14 pointwise ops per pixel
+    (kernels.py:146-152: mul, add, rsqrt, mul, clamp, mul, sub, clamp, sqrt, acos, sub,
+    mul, add, div; a transcendental counted as one) and one add per Sum/Mixture term."""
+    f = 0
+    for op in plan.prog.ops:
+        hw = op.shape_out[0] * op.shape_out[1]
+        if op.kind == "conv":
+            f += hw
+        elif op.kind == "relu":
+            f += 14 * hw
+        elif op.kind == "add":
+            f += (len(op.terms) - 1) * hw
+    return f
+
+
 def net_roofline(model, x, cfg_name, timing):
     """Roofline of the whole-network kernel from the HIP events recorded around each of its
     launches in the timed region (cnn_gp.netplan.TIMING, on the launch stream)."""
@@ -184,6 +201,8 @@ def net_roofline(model, x, cfg_name, timing):
     pairs = sum(p for _, _, p in timing)
     fl = alg_flops_per_pair(plan)
     achieved = fl * pairs / (ms * 1e-3) / 1e12
+    fl_pw = fl + alg_flops_pointwise_per_pair(plan)
+    achieved_pw = fl_pw * pairs / (ms * 1e-3) / 1e12
     traffic = None
     try:
         with open(TRAFFIC_FILE) as f:
@@ -199,6 +218,9 @@ def net_roofline(model, x, cfg_name, timing):
             "kernel": kname, "launches": len(timing), "avg_ms": round(ms / len(timing), 4),
             "pairs_per_launch": pairs // len(timing), "alg_flops_per_pair": fl,
             "alg_flops_per_launch": fl * pairs // len(timing),
+            "alg_flops_incl_pointwise_per_pair": fl_pw,
+            "achieved_incl_pointwise": round(achieved_pw, 2),
+            "frac_incl_pointwise": round(achieved_pw / FP64_PEAK_TFLOPS, 4),
             "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
             "stages": [{"pairs_per_workgroup": st.pairs, "ops": st.n_ops} for st in net.stages],
             "note": "fp64 compute roof (VALU = MFMA = 78.6 TF on MI355X); algorithmic "

@@ -165,7 +165,7 @@ class NetPlan:
                     last[s_] = idx
         last[vf] = len(lowered)
         # 4. stages, then each stage's slots and records
-        multi = stages and itemsize == 8 and not plan.flags & N.CGP_FLAG_EXACT_RELU
+        multi = stages and not plan.flags & N.CGP_FLAG_EXACT_RELU
         bounds = self._stage_bounds(lowered, multi)
         self.stages = []
         for sidx, (lo, hi, np_) in enumerate(bounds):

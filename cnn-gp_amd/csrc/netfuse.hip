@@ -831,8 +831,8 @@ inline int net_wpe(long long lds_bytes) {
 }
 
 // the instantiation for (EX, DU, pairs, LDS footprint of the workgroup): the fp64 closed
-// form — the production path — has a register target per occupancy level and the
-// multi-pair stages; the exact ReLU and fp32 run one pair per workgroup
+// form — the production path — has a register target per occupancy level; fp32 one per
+// (DU, pairs); the exact ReLU runs one pair per workgroup
 template <typename T, int NP>
 const void* net_fn_np(bool du, long long lds_bytes) {
     switch (net_wpe(lds_bytes)) {
@@ -859,9 +859,16 @@ const void* net_fn(bool ex, bool du, int np, long long lds_bytes) {
         default: return nullptr;
         }
     }
-    if (np != 1) return nullptr;
-    return du ? (const void*)net_kernel<T, false, true, 4, 1>
-              : (const void*)net_kernel<T, false, false, 5, 1>;
+    // fp32: one register target per (DU, pairs)
+    switch (np) {
+    case 1: return du ? (const void*)net_kernel<T, false, true, 4, 1>
+                      : (const void*)net_kernel<T, false, false, 5, 1>;
+    case 4: return du ? (const void*)net_kernel<T, false, true, 4, 4>
+                      : (const void*)net_kernel<T, false, false, 5, 4>;
+    case 16: return du ? (const void*)net_kernel<T, false, true, 4, 16>
+                       : (const void*)net_kernel<T, false, false, 5, 16>;
+    default: return nullptr;
+    }
 }
 
 int net_occupancy(const void* fn, int lds_bytes) {
