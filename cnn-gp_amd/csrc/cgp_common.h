@@ -62,8 +62,9 @@ __host__ __device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) 
 //
 // relu_fast is the same map in closed form.  With a = |rho| = |c|/sqrt(t) (clamped) and
 // x = (1 - a)/2, acos a = 2 asin sqrt(x) turns (sqrt(t - c²) + (π - acos rho)·c)/2π into
-//     max(c, 0)/2 + sqrt(t) · x · sqrt(x) · P(4x - 1)
-// with P analytic on [0, 1/2] (tools/fit_relu_poly.py; relu_poly.h: degree 15, 3e-15).
+//     max(c, 0)/2 + sqrt(t) · x · sqrt(x) · P(x)
+// with P analytic on [0, 1/2] (tools/fit_relu_poly.py; relu_poly.h: monomials in x,
+// degree 13, 1.6e-14 relative).
 // One branch-free polynomial, two hardware rsq's refined by Newton steps, no division:
 // ~35 double ops instead of ~190 slots for correctly rounded div/sqrt/acos.  Near
 // |rho| = 1 the reference's own acos(rho) is ill-conditioned (~1e-8 relative noise from
@@ -114,16 +115,25 @@ __device__ __forceinline__ double rsqrt_fast(double t) {
     return __builtin_fma(0.5 * y, e, y);
 }
 __device__ __forceinline__ float rsqrt_fast(float t) { return __builtin_amdgcn_rsqf(t); }
-__device__ __forceinline__ double relu_poly(double u) {
+// sqrt(x) from the hardware rsqrt estimate r: s0 = x·r, then one Newton step for the
+// root itself, s = s0 + (r/2)(x - s0²) — 4 ops after the rsq instead of 5 for refining
+// r and multiplying; same accuracy (the estimate's 5e-8 squares away)
+__device__ __forceinline__ double sqrt_fast(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    const double s0 = x * r;
+    return __builtin_fma(0.5 * r, __builtin_fma(-s0, s0, x), s0);
+}
+__device__ __forceinline__ float sqrt_fast(float x) { return x * __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ double relu_poly(double x) {
     double r = kReluPolyD[kReluPolyDegD];
 #pragma unroll
-    for (int k = kReluPolyDegD - 1; k >= 0; --k) r = __builtin_fma(r, u, kReluPolyD[k]);
+    for (int k = kReluPolyDegD - 1; k >= 0; --k) r = __builtin_fma(r, x, kReluPolyD[k]);
     return r;
 }
-__device__ __forceinline__ float relu_poly(float u) {
+__device__ __forceinline__ float relu_poly(float x) {
     float r = kReluPolyF[kReluPolyDegF];
 #pragma unroll
-    for (int k = kReluPolyDegF - 1; k >= 0; --k) r = __builtin_fmaf(r, u, kReluPolyF[k]);
+    for (int k = kReluPolyDegF - 1; k >= 0; --k) r = __builtin_fmaf(r, x, kReluPolyF[k]);
     return r;
 }
 __device__ __forceinline__ double fmin_t(double a, double b) { return __builtin_fmin(a, b); }
@@ -146,9 +156,9 @@ __device__ __forceinline__ float fma_t(float a, float b, float c) {
 static __constant__ double kReluPolyTabD[kReluPolyDegD + 1] = {
 #define CGP_C(k) kReluPolyD[k]
     CGP_C(0), CGP_C(1), CGP_C(2), CGP_C(3), CGP_C(4), CGP_C(5), CGP_C(6), CGP_C(7),
-    CGP_C(8), CGP_C(9), CGP_C(10), CGP_C(11), CGP_C(12), CGP_C(13), CGP_C(14), CGP_C(15)};
+    CGP_C(8), CGP_C(9), CGP_C(10), CGP_C(11), CGP_C(12), CGP_C(13)};
 #undef CGP_C
-static_assert(kReluPolyDegD == 15, "kReluPolyTabD lists 16 coefficients");
+static_assert(kReluPolyDegD == 13, "kReluPolyTabD lists 14 coefficients");
 
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
@@ -166,13 +176,13 @@ __device__ __forceinline__ double fma_sc(double r, double u, double c) {
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(u), "s"(c));
     return o;
 }
-__device__ __forceinline__ double relu_poly(double u, const PolyTab& t) {
-    double r = fma_sc(t.d[kReluPolyDegD], u, t.d[kReluPolyDegD - 1]);
+__device__ __forceinline__ double relu_poly(double x, const PolyTab& t) {
+    double r = fma_sc(t.d[kReluPolyDegD], x, t.d[kReluPolyDegD - 1]);
 #pragma unroll
-    for (int k = kReluPolyDegD - 2; k >= 0; --k) r = fma_sc(r, u, t.d[k]);
+    for (int k = kReluPolyDegD - 2; k >= 0; --k) r = fma_sc(r, x, t.d[k]);
     return r;
 }
-__device__ __forceinline__ float relu_poly(float u, const PolyTab&) { return relu_poly(u); }
+__device__ __forceinline__ float relu_poly(float x, const PolyTab&) { return relu_poly(x); }
 
 // The same map, trimmed for the whole-network kernel (39 instead of 45 VALU ops):
 // t in one rounding (fma), 0.5·max(c, 0) as 0.25·(c + |c|) — exact, and NaN in c
@@ -184,9 +194,8 @@ __device__ __forceinline__ T relu_fast(T c, T v1, T v2, const PolyTab& tab) {
     const T st = t * y;                                     // sqrt(t)
     const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
     const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
-    const T xs = fmax_t(x, K<T>::xfloor);
-    const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
-    const T p = relu_poly(fma_t(T(-2), a, T(1)), tab);      // P(4x - 1)
+    const T sx = sqrt_fast(fmax_t(x, K<T>::xfloor));        // sqrt(x)
+    const T p = relu_poly(x, tab);                          // P(x)
     const T hpos = (c + fabs_t(c)) * T(0.25);               // max(c, 0) / 2
     return fma_t((st * x) * sx, p, hpos);
 }
@@ -198,7 +207,7 @@ __device__ __forceinline__ T relu_fast(T c, T v1, T v2, const PolyTab& tab) {
 template <int R>
 __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R],
                                             const double (&v2)[R], const PolyTab& tab) {
-    double y[R], st[R], a[R], sx[R], u[R], p[R];
+    double y[R], st[R], a[R], sx[R], u[R], p[R];   // u: x
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const double t = __builtin_fma(v1[r], v2[r], K<double>::tiny);
@@ -208,10 +217,8 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         a[r] = __builtin_fmin(__builtin_fabs(c[r] * y[r]), 1.0);
-        const double x = __builtin_fma(-0.5, a[r], 0.5);
-        const double xs = __builtin_fmax(x, K<double>::xfloor);
-        sx[r] = (st[r] * x) * (xs * rsqrt_fast(xs));
-        u[r] = __builtin_fma(-2.0, a[r], 1.0);
+        u[r] = __builtin_fma(-0.5, a[r], 0.5);
+        sx[r] = (st[r] * u[r]) * sqrt_fast(__builtin_fmax(u[r], K<double>::xfloor));
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) p[r] = fma_sc(tab.d[kReluPolyDegD], u[r], tab.d[kReluPolyDegD - 1]);
@@ -239,9 +246,8 @@ __device__ __forceinline__ T relu_fast(T c, T v1, T v2) {
     const T st = t * y;                                     // sqrt(t)
     const T a = fmin_t(fabs_t(c * y), T(1));                // |rho| clamped
     const T x = fma_t(T(-0.5), a, T(0.5));                  // (1 - a)/2
-    const T xs = fmax_t(x, K<T>::xfloor);
-    const T sx = xs * rsqrt_fast(xs);                       // sqrt(x)
-    const T p = relu_poly(fma_t(T(4), x, T(-1)));
+    const T sx = sqrt_fast(fmax_t(x, K<T>::xfloor));        // sqrt(x)
+    const T p = relu_poly(x);
     const T pos = fmax_t(c, T(0));
     // (c - c): 0 for finite c, NaN for NaN c — keeps the reference's NaN propagation
     return fma_t((st * x) * sx, p, T(0.5) * pos) + (c - c);

@@ -473,6 +473,11 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
+                // the variances are first needed here: without this fence the compiler
+                // folds u1·u2 (the ReLU's t) into the load block at the op start and
+                // waits for the loads there, before the row pass
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k) asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
                 T o[G::R3], v[G::R3];
                 win_sums<T, G::TAPS, G::S, G::R3>(win, o);
                 int at[G::R3];
