@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import os
 from typing import Optional
 
 import torch
@@ -39,6 +40,11 @@ ALIGN = 2                      # slot bases on 16-byte boundaries (fp64 elements
 # Optional launch timing (bench.py): when a list, every launch appends
 # (start event, end event, pairs evaluated) recorded on the launch stream.
 TIMING = None
+
+# Run the library's compiled program for an op list when it holds one (cgp_net_program:
+# the reference configs' lowered programs, every offset an immediate).  False forces the
+# op-record interpreter (A/B and parity tests of both paths).
+USE_PROGRAMS = os.environ.get("CGP_NET_PROGRAMS", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
 
 
@@ -526,7 +532,8 @@ class NetPlan:
             for b in range(1, len(self.stages)):
                 states[b] = torch.empty((chunk * self.stages[b].load_stride,),
                                         dtype=x.dtype, device=x.device)
-        fn = getattr(N.load(), f"cgp_net_{sfx}")
+        lib = N.load()
+        fn = getattr(lib, f"cgp_net_{sfx}")
         launches = []
         keep = []
         for sidx, st in enumerate(self.stages):
@@ -545,6 +552,9 @@ class NetPlan:
             a.flags = flags | (N.CGP_FLAG_NET_DUAL if st.dual else 0)
             a.pairs = st.pairs
             a.final_stage = int(st.final)
+            a.program = lib.cgp_net_program(ctypes.byref(arr), st.n_ops, st.pairs, a.flags,
+                                            st.lds_elems, x.element_size()) \
+                if USE_PROGRAMS else 0
             launches.append(a)
 
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2

@@ -755,11 +755,101 @@ __device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op
     }
 }
 
+// ---- compiled programs ------------------------------------------------------------
+// The lowered op lists of the reference configs (tools/gen_net_programs.py ->
+// net_programs.h).  A program kernel runs its ops as straight-line code: kind, geometry,
+// LDS offsets and strides are immediates, only weight / bias / variance pointers are read
+// from the launch's op records.  The host picks it with cgp_net_program().
+struct ProgOp {
+    int kind, code, src, dst, add, ws_in, ws_out, relu, h, w, dst2, zero_halo;
+};
+struct ProgInfo {
+    int first, nops, pairs, dual, lds_elems, sizes;
+};
+#include "net_programs.h"
+constexpr int kNumProgs = sizeof(kProgs) / sizeof(kProgs[0]);
+
+template <typename T, bool DU, int NP, int PID, int K>
+__device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, const Pairs& pr,
+                                         int tid) {
+    constexpr ProgInfo I = kProgs[PID];
+    if constexpr (K < I.nops) {
+        constexpr ProgOp o = kProgOps[I.first + K];
+        const cgp_net_op& rt = p.ops[K];
+        cgp_net_op op;
+        op.kind = o.kind;
+        op.code = o.code;
+        op.src = o.src;
+        op.dst = o.dst;
+        op.add = o.add;
+        op.ws_in = o.ws_in;
+        op.ws_out = o.ws_out;
+        op.relu = o.relu;
+        op.h = o.h;
+        op.w = o.w;
+        op.div_m = 0;
+        op.div_s = 0;
+        op.dst2 = o.dst2;
+        op.zero_halo = o.zero_halo;
+        op.weight = rt.weight;
+        op.bias = rt.bias;
+        op.var_x = rt.var_x;
+        op.var_y = rt.var_y;
+        op.var2_x = rt.var2_x;
+        op.var2_y = rt.var2_y;
+        if constexpr (o.zero_halo != 0) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const int qa = q * I.lds_elems;
+                zero_halos(lds + qa, o.dst, o.zero_halo & 0xffff, o.h, o.w, o.ws_out, tid);
+                zero_halos(lds + qa, o.dst2, (unsigned)o.zero_halo >> 16, o.h, o.w, o.ws_out,
+                           tid);
+            }
+        }
+        if constexpr (o.kind == CGP_NET_CONV) {
+            constexpr GeoRow g = kGeoTable[o.code];
+            net_conv<T, false, DU, NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>>(lds, op, p,
+                                                                                    pr);
+        } else if constexpr (o.kind == CGP_NET_RELU || o.kind == CGP_NET_LINEAR ||
+                             o.kind == CGP_NET_MOMENTS) {
+            net_elem<T, false, DU, o.kind, o.h, o.w, NP>(lds, op, p, pr);
+        } else if constexpr (o.kind == CGP_NET_LOAD || o.kind == CGP_NET_STORE) {
+            net_move<T, o.kind, NP>(lds, op, p, pr);
+        }
+        lds_barrier();
+        prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid);
+    }
+}
+
+// the compiled program whose op list equals ops[0, nops) field by field (host memory), +1;
+// 0 if none
+int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_elems,
+               int itemsize) {
+    for (int k = 0; k < kNumProgs; ++k) {
+        const ProgInfo& I = kProgs[k];
+        if (I.nops != nops || I.pairs != pairs || I.dual != dual || I.lds_elems != lds_elems ||
+            !(I.sizes & itemsize))
+            continue;
+        bool eq = true;
+        for (int n = 0; n < nops && eq; ++n) {
+            const ProgOp& o = kProgOps[I.first + n];
+            const cgp_net_op& r = ops[n];
+            eq = o.kind == r.kind && o.code == r.code && o.src == r.src && o.dst == r.dst &&
+                 o.add == r.add && o.ws_in == r.ws_in && o.ws_out == r.ws_out &&
+                 o.relu == r.relu && o.h == r.h && o.w == r.w && o.dst2 == r.dst2 &&
+                 o.zero_halo == r.zero_halo;
+        }
+        if (eq) return k + 1;
+    }
+    return 0;
+}
+
 // WPE: waves per SIMD the register allocation targets (amdgpu_waves_per_eu).  LDS caps
 // the resident workgroups per CU (two waves each) at 160 KB / footprint, so allocating
 // registers for more waves than that only forces spills; net_launch picks WPE from the
 // LDS footprint (net_wpe).  NP: pairs per workgroup (1, or 4 / 16 for small-map stages).
-template <typename T, bool EX, bool DU, int WPE, int NP>
+// PID >= 0: compiled program PID instead of the op-record interpreter.
+template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     __shared__ unsigned pair_tab[2 * kMaxNP];
@@ -798,10 +888,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
             pr.i = pr.j = 0;
             lds_barrier();
         }
-        for (int k = 0; k < p.nops; ++k) {
-            const cgp_net_op op = p.ops[k];
-            net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
-            lds_barrier();
+        if constexpr (PID < 0) {
+            for (int k = 0; k < p.nops; ++k) {
+                const cgp_net_op op = p.ops[k];
+                net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
+                lds_barrier();
+            }
+        } else {
+            prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid);
         }
         if (p.final_stage) {
             if constexpr (NP == 1) {
@@ -829,7 +923,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 // waves per SIMD the LDS footprint allows (kNT / 64 waves per workgroup, 4 SIMDs per CU),
 // clamped to the instantiated register targets 3..5
-inline int net_wpe(long long lds_bytes) {
+constexpr int net_wpe(long long lds_bytes) {
     const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
     const long long w = wg * (kNT / 64) / 4;
     return w < 3 ? 3 : (w > 5 ? 5 : (int)w);
@@ -876,6 +970,29 @@ const void* net_fn(bool ex, bool du, int np, long long lds_bytes) {
     }
 }
 
+// program kernels: fp64 register target from the program's LDS footprint, fp32 as net_fn
+template <typename T, int PID>
+const void* prog_fn_one() {
+    constexpr ProgInfo I = kProgs[PID];
+    if constexpr ((I.sizes & (int)sizeof(T)) == 0) {
+        return nullptr;
+    } else {
+        constexpr long long bytes = (long long)I.lds_elems * (long long)sizeof(T) * I.pairs;
+        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes) : (I.dual ? 4 : 5);
+        return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
+    }
+}
+template <typename T>
+const void* prog_fn(int pid) {
+    switch (pid) {
+#define CGP_PROG_CASE(k) \
+    case k: return prog_fn_one<T, k>();
+        CGP_NET_PROGRAMS(CGP_PROG_CASE)
+#undef CGP_PROG_CASE
+    default: return nullptr;
+    }
+}
+
 int net_occupancy(const void* fn, int lds_bytes) {
     if (lds_bytes > 64 * 1024 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
@@ -899,9 +1016,10 @@ int net_occupancy_for(int lds_bytes, int flags, int np) {
 }
 
 template <typename T>
-int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, void* stream) {
+int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, int program,
+               void* stream) {
     const long long wg_bytes = lds_bytes * np;
-    const void* fn = net_fn<T>(ex, du, np, wg_bytes);
+    const void* fn = program > 0 && !ex ? prog_fn<T>(program - 1) : net_fn<T>(ex, du, np, wg_bytes);
     if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
     const int per_cu = net_occupancy(fn, (int)wg_bytes);
     if (per_cu <= 0)
@@ -976,7 +1094,16 @@ int net_impl(const cgp_net_args* a, void* stream) {
                     (long long)p.uend, (long long)p.units);
     p.final_stage = a->final_stage;
     const bool du = (a->flags & CGP_FLAG_NET_DUAL) != 0;
-    return net_launch<T>(p, p.exact != 0, du, np, lds_bytes, stream);
+    const int prog = a->program;
+    if (prog < 0 || prog > kNumProgs)
+        return fail(CGP_EINVAL, "net: program %d of %d", prog, kNumProgs);
+    if (prog > 0) {
+        const ProgInfo& I = kProgs[prog - 1];
+        if (I.nops != a->nops || I.pairs != np || I.dual != (du ? 1 : 0) ||
+            I.lds_elems != a->lds_elems || !(I.sizes & (int)sizeof(T)))
+            return fail(CGP_EINVAL, "net: program %d does not fit this op list", prog);
+    }
+    return net_launch<T>(p, p.exact != 0, du, np, lds_bytes, prog, stream);
 }
 
 }  // namespace
@@ -1008,6 +1135,13 @@ int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pai
     if (lds_bytes <= 0 || (long long)lds_bytes * pairs > 160 * 1024) return 0;
     return f64 ? net_occupancy_for<double>(lds_bytes, flags, pairs)
                : net_occupancy_for<float>(lds_bytes, flags, pairs);
+}
+
+int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t flags,
+                    int32_t lds_elems, int32_t itemsize) {
+    if (!ops || nops <= 0) return 0;
+    return prog_match(ops, nops, pairs <= 0 ? 1 : pairs, (flags & CGP_FLAG_NET_DUAL) ? 1 : 0,
+                      lds_elems, itemsize);
 }
 
 int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 4
+#define CGP_ABI_VERSION 5
 
 /* error codes */
 #define CGP_OK 0
@@ -268,7 +268,8 @@ typedef struct cgp_net_args {
     int64_t unit_begin;    /* the tile's pair units this launch covers, [begin, end): unit */
     int64_t unit_end;      /* u = 64·supertile + 8·(i % 8) + j % 8; 0, 0 = the whole tile */
     int32_t final_stage;   /* 1: write K (the last stage); 0: the ops end in CGP_NET_STORE */
-    int32_t reserved2;
+    int32_t program;       /* 0: interpret the op records; k > 0: run compiled program k,
+                              the value cgp_net_program() returned for these records */
 } cgp_net_args;
 
 /* Geometry code of a conv for CGP_NET_CONV, or -1 if the fused kernel has no
@@ -287,6 +288,13 @@ int cgp_net_resolution(int32_t h, int32_t w);
 /* workgroups per CU the fused kernel reaches with lds_bytes of LDS per pair and `pairs`
  * pairs per workgroup (0 if it cannot run) */
 int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs);
+/* The compiled program (k > 0) whose op list equals ops[0, nops) (HOST memory) in every
+ * field but weight, bias and the variance / state pointers, for `pairs` pairs per
+ * workgroup, flags (CGP_FLAG_NET_DUAL), the per-pair LDS footprint and the item size
+ * (4 or 8); 0 if none.  The library holds the lowered programs of the reference configs
+ * (net_programs.h); a program kernel runs them with every offset an immediate. */
+int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t flags,
+                    int32_t lds_elems, int32_t itemsize);
 int cgp_net_f64(const cgp_net_args* args, void* stream);
 int cgp_net_f32(const cgp_net_args* args, void* stream);
 

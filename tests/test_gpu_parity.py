@@ -334,6 +334,38 @@ def test_netfuse_matches_layer_path(cfg, dtn, same):
         assert np.array_equal(a, a.T)
 
 
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("dtn", ["f64", "f32"])
+@pytest.mark.parametrize("same", [True, False])
+def test_compiled_program_equals_interpreter(cfg, dtn, same, monkeypatch):
+    """the compiled program kernel (net_programs.h) and the op-record interpreter run the
+    same arithmetic in the same order: identical results, bit for bit; a model with other
+    weights (same architecture) still runs the program"""
+    from cnn_gp import netplan
+    rng = np.random.default_rng(12)
+    C, side = specs.GEOMETRY[cfg]
+    tdt = torch.float64 if dtn == "f64" else torch.float32
+    X = dev(rng.random((13, C, side, side)), tdt)
+    Z = dev(rng.random((10, C, side, side)), tdt)
+    m = configs_util.model(cfg).to(DEV, tdt)
+    with torch.no_grad():
+        for mod in m.modules():                # other weights: not part of the program
+            if isinstance(mod, cnn_gp.Conv2d):
+                mod.var_weight = mod.var_weight * 1.3
+        picked = []
+        real = N.load().cgp_net_program
+
+        def spy(*a):
+            picked.append(real(*a))
+            return picked[-1]
+        monkeypatch.setattr(N.load(), "cgp_net_program", spy, raising=False)
+        a = (m(X) if same else m(X, Z, False, False)).cpu().numpy()
+        assert picked and all(p > 0 for p in picked), picked
+        monkeypatch.setattr(netplan, "USE_PROGRAMS", False)
+        b = (m(X) if same else m(X, Z, False, False)).cpu().numpy()
+    assert np.array_equal(a, b), rel_err(a, b)
+
+
 @pytest.mark.parametrize("n1,n2", [(1, 1), (1, 9), (9, 1), (7, 17), (17, 8), (8, 8)])
 def test_netfuse_ragged_tiles_vs_oracle(n1, n2):
     """supertile walk: sizes that are not multiples of the 8x8 pair block"""

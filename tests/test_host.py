@@ -271,3 +271,66 @@ def test_bench_balanced_split_covers_every_tile_once():
         cost = lambda t: B * (B - 1) // 2 if t[0] else B * B  # noqa: E731
         loads = [sum(cost(t) for t in p) for p in parts]
         assert max(loads) - sum(loads) / world <= B * B
+
+
+# ------------------------------------------------------------------------------------
+# compiled programs (csrc/net_programs.h, tools/gen_net_programs.py)
+# ------------------------------------------------------------------------------------
+def _stage_program_ids(name, dt):
+    import importlib
+    from cnn_gp import netplan
+    cfg = importlib.import_module(f"configs.{name}")
+    m = cfg.initial_model.to(dt)
+    side = 32 if getattr(cfg, "in_channels", 1) == 3 else 28
+    plan = m._plan(side, side)
+    itemsize = torch.tensor([], dtype=dt).element_size()
+    net = m._net_plan(plan, itemsize)
+    dummy = torch.zeros(8, dtype=torch.float64)
+    var = {v: (dummy, dummy) for v in net.need_var}
+    ids = []
+    for st in net.stages:
+        arr = net._ops_array(st, var, dummy, dummy)
+        flags = N.CGP_FLAG_NET_DUAL if st.dual else 0
+        ids.append(N.load().cgp_net_program(ctypes.byref(arr), st.n_ops, st.pairs, flags,
+                                            st.lds_elems, itemsize))
+    return ids, net
+
+
+@pytest.mark.parametrize("name", ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp",
+                                  "mnist_as_tf", "cifar10"])
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_reference_configs_have_compiled_programs(name, dt):
+    """net_programs.h is in sync with NetPlan's lowering: every stage of every reference
+    config finds its compiled program (a stale header would silently fall back to the
+    interpreter; rerun tools/gen_net_programs.py)"""
+    ids, _ = _stage_program_ids(name, dt)
+    assert all(i > 0 for i in ids), ids
+    assert len(set(ids)) == len(ids)
+
+
+def test_program_match_ignores_weights_but_not_structure():
+    """weights, biases and variance pointers are runtime fields; any structural field
+    (here one LDS offset) makes the op list fall back to the interpreter"""
+    import importlib
+    cfg = importlib.import_module("configs.mnist_paper_convnet_gp")
+    m = cfg.initial_model.double()
+    net = m._net_plan(m._plan(28, 28), 8)
+    st = net.stages[0]
+    dummy = torch.zeros(8, dtype=torch.float64)
+    var = {v: (dummy, dummy) for v in net.need_var}
+    arr = net._ops_array(st, var)
+    lib = N.load()
+    pid = lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8)
+    assert pid > 0
+    for o in arr:
+        o.weight, o.bias = 3.5, 0.25
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8) == pid
+    arr[3].dst += 1
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8) == 0
+    arr[3].dst -= 1
+    # other pair count, dual flag, footprint or item size: no program
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 4, 0, st.lds_elems, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, N.CGP_FLAG_NET_DUAL,
+                               st.lds_elems, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems + 2, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops - 1, 1, 0, st.lds_elems, 8) == 0
