@@ -75,7 +75,13 @@ struct NG {
     static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NP * NH + kNT - 1) / kNT;
     static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NP * NV + kNT - 1) / kNT;
     static constexpr int NZ = (HSR - NVR) * WO;                // zero cells of hs
-    static constexpr int HS_ELEMS = (POINT || REDUCE) ? 2 : HSR * WO;
+    // windows of at most 3 taps (the ResNets' 3x3 convs) run in one pass straight from the
+    // source slot: no row-sum scratch, so a smaller arena (CGP_NET_DIRECT=0: separable)
+#ifndef CGP_NET_DIRECT
+#define CGP_NET_DIRECT 1
+#endif
+    static constexpr bool DIRECT = CGP_NET_DIRECT && !POINT && !REDUCE && TAPS <= 3;
+    static constexpr int HS_ELEMS = (POINT || REDUCE || DIRECT) ? 2 : HSR * WO;
 };
 
 // The fused kernel's conv shapes: (H, W, HO, WO, taps, stride, offset) — every conv of the
@@ -405,6 +411,80 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
         net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
+    } else if constexpr (G::DIRECT) {
+        // one pass: item (q, g3, c) sums its WIN3 x TAPS input window straight from the
+        // source slot (row sums, then column sums: the separable path's order, so the
+        // same bits); rows outside the map read as zero, columns outside are the slot's
+        // zero halo
+        constexpr int NVT = NP * G::NV;
+        T u1[G::KV][G::R3], u2[G::KV][G::R3];
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv) {
+            const int it = tid + kv * kNT;
+            const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
+            const int q = NP == 1 ? 0 : itc / G::NV, l = itc - q * G::NV;
+            const int g3 = l / G::WO, c = l - g3 * G::WO;
+            const VarSrc<T> vs = vs_of(q);
+#pragma unroll
+            for (int k = 0; k < G::R3; ++k) {
+                u1[kv][k] = vs.on ? vs.x[(g3 * G::R3 + k) * G::WO + c] : T(1);
+                u2[kv][k] = vs.on ? vs.y[(g3 * G::R3 + k) * G::WO + c] : T(1);
+            }
+        }
+        // outputs that land on the source (in place, or dst2 on the source) are stored
+        // after every item has read its window
+        const int s_lo = op.src - wsi, s_hi = op.src + G::H * wsi;
+        auto hits = [&](int d) {
+            return d >= 0 && d - wso < s_hi && d + G::HO * wso > s_lo;
+        };
+        const bool hazard = hits(op.dst) || (DU && hits(op.dst2));
+        T res[G::KV][G::R3];
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv) {
+            const int it = tid + kv * kNT;
+            if (NVT % kNT == 0 || it < NVT) {
+                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
+                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const T* base = src + q * arena + c * G::S + G::OFF;
+                const int r0 = g3 * G::R3 * G::S + G::OFF;
+                T rs[G::WIN3];
+#pragma unroll
+                for (int t = 0; t < G::WIN3; ++t) {
+                    const bool lo = G::OFF + t < 0, hi = (G::NG3 - 1) * G::R3 * G::S + G::OFF + t >= G::H;
+                    const int r = r0 + t;
+                    const bool in = (!lo || r >= 0) && (!hi || r < G::H);
+                    const T* row = base + (in ? r : 0) * wsi;
+                    T a = row[0];
+#pragma unroll
+                    for (int dx = 1; dx < G::TAPS; ++dx) a += row[dx];
+                    rs[t] = in ? a : T(0);
+                }
+                T o[G::R3];
+                win_sums<T, G::TAPS, G::S, G::R3>(rs, o);
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k) res[kv][k] = fma_t(w, o[k], b);
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k)
+                    asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
+            }
+        }
+        if (hazard) lds_barrier();
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv) {
+            const int it = tid + kv * kNT;
+            if (NVT % kNT == 0 || it < NVT) {
+                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
+                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                int at[G::R3];
+                bool ok[G::R3];
+#pragma unroll
+                for (int k = 0; k < G::R3; ++k) {
+                    at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
+                    ok[k] = true;
+                }
+                net_out<T, EX, DU, G::R3>(lds, op, res[kv], at, ok, u1[kv], u2[kv], tab);
+            }
+        }
     } else {
         T* __restrict__ hs = lds + p.hs;
         constexpr int NHT = NP * G::NH, NVT = NP * G::NV, NZT = NP * G::NZ;
@@ -939,8 +1019,9 @@ const void* net_fn_np(bool du, long long lds_bytes) {
                       : (const void*)net_kernel<T, false, false, 3, NP>;
     case 4: return du ? (const void*)net_kernel<T, false, true, 4, NP>
                       : (const void*)net_kernel<T, false, false, 4, NP>;
-    default: return du ? (const void*)net_kernel<T, false, true, 5, NP>
-                       : (const void*)net_kernel<T, false, false, 5, NP>;
+    default:   // the interpreter's dual-output instantiation spills at 5 waves: 4
+        return du ? (const void*)net_kernel<T, false, true, 4, NP>
+                  : (const void*)net_kernel<T, false, false, 5, NP>;
     }
 }
 template <typename T>
