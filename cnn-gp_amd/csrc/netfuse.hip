@@ -1003,11 +1003,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 // waves per SIMD the LDS footprint allows (kNT / 64 waves per workgroup, 4 SIMDs per CU),
 // clamped to the instantiated register targets 3..5
-constexpr int net_wpe(long long lds_bytes) {
+constexpr int net_wpe(long long lds_bytes, int cap = 5) {
     const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
     const long long w = wg * (kNT / 64) / 4;
-    return w < 3 ? 3 : (w > 5 ? 5 : (int)w);
+    return w < 3 ? 3 : (w > cap ? cap : (int)w);
 }
+#ifndef CGP_NET_PROG_WPE_MAX
+#define CGP_NET_PROG_WPE_MAX 5
+#endif
 
 // the instantiation for (EX, DU, pairs, LDS footprint of the workgroup): the fp64 closed
 // form — the production path — has a register target per occupancy level; fp32 one per
@@ -1059,7 +1062,7 @@ const void* prog_fn_one() {
         return nullptr;
     } else {
         constexpr long long bytes = (long long)I.lds_elems * (long long)sizeof(T) * I.pairs;
-        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes) : (I.dual ? 4 : 5);
+        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX) : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
 }
