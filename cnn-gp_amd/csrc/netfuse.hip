@@ -21,6 +21,9 @@
 
 #include "cgp_common.h"
 
+#include <atomic>
+#include <mutex>
+
 #include <algorithm>
 #include <climits>
 
@@ -202,6 +205,7 @@ struct NetP {
     T* __restrict__ out;
     const T* __restrict__ kdiag;
     const cgp_net_op* __restrict__ ops;
+    unsigned long long* work;   // per-XCD unit counters (CGP_NET_DYN), zeroed per launch
     long long ldo, units, ubeg, uend;
     unsigned n1, n2, nbi, nbj;
     int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact, final_stage;
@@ -928,6 +932,9 @@ int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_ele
 // the resident workgroups per CU (two waves each) at 160 KB / footprint, so allocating
 // registers for more waves than that only forces spills; net_launch picks WPE from the
 // LDS footprint (net_wpe).  NP: pairs per workgroup (1, or 4 / 16 for small-map stages).
+#ifndef CGP_NET_DYN
+#define CGP_NET_DYN 1
+#endif
 // PID >= 0: compiled program PID instead of the op-record interpreter.
 template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
@@ -945,7 +952,29 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const long long per = ((span + 7) / 8 + NP - 1) / NP * NP;
     const long long beg = p.ubeg + (long long)xcd * per;
     const long long end = beg + per < p.uend ? beg + per : p.uend;
+#if CGP_NET_DYN
+    // the XCD's workgroups take its units in order from one counter, so the pairs in
+    // flight on an XCD stay one contiguous window (a few supertiles) whose images and
+    // variance maps its L2 holds; a static stride lets workgroups drift apart and the
+    // window (and L2 misses) grow.  The next group's index is fetched one pair ahead.
+    __shared__ long long next_u;
+    unsigned long long* ctr = p.work + xcd;
+    (void)g8;
+    (void)l;
+    unsigned long long grab = 0;   // thread 0: the counter value fetched one pair ahead
+    if (tid == 0) grab = atomicAdd(ctr, 1ull);
+    auto advance = [&]() {
+        if (tid == 0) next_u = beg + (long long)grab * NP;
+        lds_barrier();
+        const long long v = next_u;
+        lds_barrier();
+        return v;
+    };
+    for (long long u = advance(); u < end; u = advance()) {
+        if (tid == 0) grab = atomicAdd(ctr, 1ull);
+#else
     for (long long u = beg + (long long)l * NP; u < end; u += (long long)g8 * NP) {
+#endif
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
@@ -1099,6 +1128,34 @@ int net_occupancy_for(int lds_bytes, int flags, int np) {
     return fn ? net_occupancy(fn, lds_bytes * np) : 0;
 }
 
+// Per-XCD unit counters for a launch: slots of 8 counters rotate through one device
+// buffer (a slot is reused 64 launches later, long after its launch has drained) and are
+// zeroed on the launch stream.
+unsigned long long* work_counters(void* stream) {
+    constexpr int kSlots = 64, kDevices = 64;
+    static std::mutex mu;
+    static unsigned long long* buf[kDevices] = {};
+    static std::atomic<unsigned> next{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevices) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!buf[dev] &&
+            hipMalloc(&buf[dev], sizeof(unsigned long long) * 8 * kSlots) != hipSuccess) {
+            (void)hipGetLastError();
+            buf[dev] = nullptr;
+            return nullptr;
+        }
+    }
+    unsigned long long* slot = buf[dev] + 8 * (next++ % kSlots);
+    if (hipMemsetAsync(slot, 0, sizeof(unsigned long long) * 8, as_stream(stream)) != hipSuccess)
+        return nullptr;
+    return slot;
+}
+
 template <typename T>
 int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, int program,
                void* stream) {
@@ -1113,6 +1170,8 @@ int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, 
     if (grid > groups) grid = groups;
     grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
     NetP<T> arg = p;
+    arg.work = work_counters(stream);
+    if (!arg.work) return fail(CGP_EHIP, "net: work counters");
     void* args[] = {&arg};
     CGP_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args, (size_t)wg_bytes,
                             as_stream(stream)));
