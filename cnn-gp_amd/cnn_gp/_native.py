@@ -111,6 +111,7 @@ SIGNATURES = {
                                   ctypes.POINTER(_i64), _vp]),
     "cgp_gemm_f64": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "cgp_pred_var_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp]),
     "cgp_net_geometry": (_i32, [_i32] * 7),
     "cgp_net_hs_elems": (_i32, [_i32]),
     "cgp_net_resolution": (_i32, [_i32, _i32]),

@@ -15,7 +15,7 @@ import torch
 from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
-           "accuracy", "one_hot_pm1")
+           "accuracy", "one_hot_pm1", "predictive_variance")
 
 
 def _device():
@@ -67,6 +67,37 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = True):
         N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
     sol = sol.reshape(n) if vec else sol
     return sol.to(Y.device)
+
+
+def predictive_variance(Kfactor, Kxz, kz_diag, overwrite_kxz: bool = False):
+    """GP posterior variance of the test points: kz_diag[t] − Kzx[t]·Kxx⁻¹·Kxz[:, t].
+
+    Kfactor: the device tensor ``solve_system(Kxx, Y, overwrite_a=True)`` left Kxx in
+    (its upper triangle holds U, Kxx = UᵀU; the lower triangle is never read).  Kxz:
+    [m, n] (one test point per row, as save_kernel.py stores Kxvx / Kxtx), kz_diag: [m]
+    prior variances (the Kv_diag / Kt_diag datasets, save_kernel.py:33-36, computed with
+    ``model(z, z, True, True)``).  One rocBLAS dtrsm_64 (V = U⁻ᵀ Kxz, in place) and a
+    row sum of squares, through cgp_pred_var_f64.  Kxz is overwritten with V only when it
+    is a contiguous float64 device tensor and ``overwrite_kxz``.  SURVEY.md §8f row 4;
+    the reference's classify_gp.py stops at the posterior mean (:39-42).
+    """
+    dev = Kfactor.device if Kfactor.device.type == "cuda" else _device()
+    n = Kfactor.shape[0]
+    assert Kfactor.dtype == torch.float64 and Kfactor.dim() == 2 and Kfactor.shape[1] == n
+    assert Kfactor.device == dev and Kfactor.is_contiguous(), "Kfactor: the device factor"
+    assert Kxz.dim() == 2 and Kxz.shape[1] == n, (Kxz.shape, n)
+    m = Kxz.shape[0]
+    with torch.cuda.device(dev):
+        if (overwrite_kxz and Kxz.device == dev and Kxz.dtype == torch.float64
+                and Kxz.is_contiguous()):
+            V = Kxz
+        else:
+            V = Kxz.to(dev, dtype=torch.float64).clone(memory_format=torch.contiguous_format)
+        d = torch.as_tensor(kz_diag).to(dev, dtype=torch.float64).reshape(m).contiguous()
+        var = torch.empty((m,), dtype=torch.float64, device=dev)
+        N.call("cgp_pred_var_f64", N.ptr(Kfactor), n, n, N.ptr(V), m, n, N.ptr(d), N.ptr(var),
+               _stream(dev))
+    return var
 
 
 def diag_add(K, diag):

@@ -729,6 +729,28 @@ __global__ __launch_bounds__(kBlock) void diag_add_kernel(double* k, long long n
         k[e * ld + e] += v;
 }
 
+// var[r] = d[r] − Σ_c v[r][c]² — one workgroup per row (grid-stride over rows), each
+// thread a strided partial sum, then a fixed-order LDS tree: deterministic, coalesced.
+__global__ __launch_bounds__(kBlock) void row_sumsq_sub_kernel(const double* __restrict__ v,
+                                                               long long rows, long long cols,
+                                                               long long ld,
+                                                               const double* d, double* out) {
+    __shared__ double part[kBlock];
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x) {
+        const double* row = v + r * ld;
+        double acc = 0.0;
+        for (long long c = threadIdx.x; c < cols; c += kBlock) acc = __builtin_fma(row[c], row[c], acc);
+        part[threadIdx.x] = acc;
+        __syncthreads();
+        for (int w = kBlock / 2; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[r] = d[r] - part[0];
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void argmax_rows_kernel(const double* __restrict__ a,
                                                              long long rows, long long cols,
                                                              long long* __restrict__ out) {
@@ -1253,6 +1275,34 @@ int cgp_gemm_f64(const double* a, const double* b, double* c, int64_t m, int64_t
     CGP_BLAS(rocblas_dgemm_64(h, rocblas_operation_none, rocblas_operation_none, n, m, kdim,
                               &one, b, n, a, kdim, &zero, c, n));
     return CGP_OK;
+}
+
+int cgp_pred_var_f64(const double* k, int64_t n, int64_t ldk, double* kxz, int64_t m,
+                     int64_t ldz, const double* kz_diag, double* var, void* stream) {
+    if (!k || !kxz || !kz_diag || !var) return fail(CGP_EINVAL, "pred_var: NULL argument");
+    if (n <= 0 || ldk < n || m < 0 || ldz < n)
+        return fail(CGP_EINVAL, "pred_var: bad sizes n=%lld ldk=%lld m=%lld ldz=%lld",
+                    (long long)n, (long long)ldk, (long long)m, (long long)ldz);
+    if (m == 0) return CGP_OK;
+    hipStream_t s = as_stream(stream);
+    rocblas_handle h;
+    int rc = blas_handle(&h);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_blas_mu);
+        CGP_BLAS(rocblas_set_stream(h, s));
+        CGP_BLAS(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
+        const double one = 1.0;
+        // column-major: L = the factor's lower triangle (n×n, Kxx = L·Lᵀ), B = Kxz (n×m,
+        // ld ldz).  L·V = B  <=>  V = U⁻ᵀ Kxz with U = Lᵀ the row-major upper factor.
+        CGP_BLAS(rocblas_dtrsm_64(h, rocblas_side_left, rocblas_fill_lower,
+                                  rocblas_operation_none, rocblas_diagonal_non_unit, n, m,
+                                  &one, k, ldk, kxz, ldz));
+    }
+    const unsigned grid = (unsigned)(m < 65536 ? m : 65536);
+    hipLaunchKernelGGL(row_sumsq_sub_kernel, dim3(grid), dim3(kBlock), 0, s, kxz,
+                       (long long)m, (long long)n, (long long)ldz, kz_diag, var);
+    return check_launch("row_sumsq_sub_kernel");
 }
 
 int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* out,

@@ -187,6 +187,18 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
  */
 int cgp_gemm_f64(const double* a, const double* b, double* c, int64_t m, int64_t n,
                  int64_t kdim, void* stream);
+/*
+ * GP predictive variance of m test points (the Kv_diag / Kt_diag
+ * datasets save_kernel.py:33-36 writes are the prior variances this subtracts from):
+ *   var[t] = kz_diag[t] − Kzx[t,:] · Kxx⁻¹ · Kxz[:,t]
+ * given the factor cgp_chol_solve_f64 left in k (row-major upper triangle U, Kxx = UᵀU;
+ * only that triangle is read, the NaN lower tiles of the reference's files are ignored).
+ *   kxz: Kzx as [m][ldz] row-major (one test point per row, ldz >= n) — overwritten by
+ *        V = U⁻ᵀ Kxz (rocblas_dtrsm_64, in place), so var[t] = kz_diag[t] − Σ_r V[t][r]².
+ *   kz_diag: [m] prior variances (DiagIterator output); var: [m] out (may alias kz_diag).
+ */
+int cgp_pred_var_f64(const double* k, int64_t n, int64_t ldk, double* kxz, int64_t m,
+                     int64_t ldz, const double* kz_diag, double* var, void* stream);
 /* out[r] = argmax_c a[r][c] (first maximum, like torch.argmax), a: [rows][cols] */
 int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* out,
                         void* stream);

@@ -550,6 +550,68 @@ def test_predict_and_cast():
     np.testing.assert_array_equal(out.cpu().numpy(), f32[1].astype(np.float64))
 
 
+def _joint_spd(n, m, seed):
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((n + m, n + m + 8))
+    return A @ A.T / (n + m) + 0.05 * np.eye(n + m)
+
+
+def _pred_var_ref(J, n):
+    Kxx, Kzx, kz = J[:n, :n], J[n:, :n], np.diag(J[n:, n:])
+    return kz - np.einsum("tr,rt->t", Kzx, np.linalg.solve(Kxx, Kzx.T))
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (7, 3), (300, 45), (513, 130)])
+def test_predictive_variance_vs_numpy(n, m):
+    """posterior variance from the device Cholesky factor (NaN lower triangle, as the
+    reference's HDF5 Kxx arrives) equals kz − diag(Kzx Kxx⁻¹ Kxz) in float64"""
+    J = _joint_spd(n, m, n + m)
+    K = torch.from_numpy(J[:n, :n].copy())
+    K[tuple(np.tril_indices(n, -1))] = float("nan")
+    K = K.to(DEV)
+    Y = torch.ones((n, 1), dtype=torch.float64, device=DEV)
+    cnn_gp.solve_system(K, Y)                      # K now holds the factor
+    Kxz = dev(J[n:, :n])
+    keep = Kxz.clone()
+    var = cnn_gp.predictive_variance(K, Kxz, dev(np.diag(J[n:, n:]).copy()))
+    assert torch.equal(Kxz, keep)                  # not overwritten by default
+    ref = _pred_var_ref(J, n)
+    scale = np.abs(np.diag(J[n:, n:])).max()
+    np.testing.assert_allclose(var.cpu().numpy(), ref, rtol=1e-9, atol=1e-11 * scale)
+    # in-place variant: Kxz becomes V = U^-T Kxz
+    var2 = cnn_gp.predictive_variance(K, Kxz, dev(np.diag(J[n:, n:]).copy()),
+                                      overwrite_kxz=True)
+    assert torch.equal(var, var2)
+    L = np.linalg.cholesky(J[:n, :n])
+    np.testing.assert_allclose(Kxz.cpu().numpy().T, np.linalg.solve(L, J[:n, n:]),
+                               rtol=1e-8, atol=1e-10)
+
+
+def test_predictive_variance_nngp():
+    """end to end on a ConvNet-GP kernel: Kxx, Kxz and the diag-mode prior variances of
+    the test points (save_kernel.py:33-36) -> posterior variance, vs numpy; training
+    points re-used as test points have ~zero posterior variance"""
+    m = configs_util.model("mnist_paper_convnet_gp").double().to(DEV)
+    g = torch.Generator().manual_seed(11)
+    X = torch.rand((96, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    Z = torch.cat([torch.rand((20, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV),
+                   X[:4]])
+    with torch.no_grad():
+        Kxx = m(X)
+        Kzx = m(Z, X, False, False)
+        kz = m(Z, Z, True, True)
+    Kxx_h, Kzx_h, kz_h = (t.cpu().numpy() for t in (Kxx, Kzx, kz))
+    jitter = 1e-6 * float(np.mean(np.diag(Kxx_h)))
+    cnn_gp.solve_system(Kxx, torch.ones((96, 1), dtype=torch.float64, device=DEV),
+                        jitter=jitter)
+    var = cnn_gp.predictive_variance(Kxx, Kzx, kz).cpu().numpy()
+    A = Kxx_h + jitter * np.eye(96)
+    ref = kz_h - np.einsum("tr,rt->t", Kzx_h, np.linalg.solve(A, Kzx_h.T))
+    np.testing.assert_allclose(var, ref, rtol=1e-6, atol=1e-9 * kz_h.max())
+    assert np.all(var[-4:] < 1e-4 * kz_h[-4:])
+    assert np.all(var[:20] > 0)
+
+
 @pytest.mark.parametrize("cfg", ["mnist_as_tf", "mnist_paper_convnet_gp"])
 def test_large_tile_properties(cfg, monkeypatch):
     """a 1536-image Kxx (staged program for the ResNet, state chunks of 64 supertiles):

@@ -49,6 +49,16 @@ def test_library_selftest():
     assert lib.cgp_selftest() == 0, lib.cgp_last_error()
 
 
+def test_pred_var_rejects_bad_arguments_on_host():
+    lib = N.load()
+    assert lib.cgp_pred_var_f64(None, 4, 4, None, 2, 4, None, None, None) == 1001
+    buf = (ctypes.c_double * 16)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert lib.cgp_pred_var_f64(p, 4, 3, p, 2, 4, p, p, None) == 1001     # ldk < n
+    assert lib.cgp_pred_var_f64(p, 4, 4, p, 2, 3, p, p, None) == 1001     # ldz < n
+    assert lib.cgp_pred_var_f64(p, 4, 4, p, 0, 4, p, p, None) == 0        # m = 0: no work
+
+
 def test_device_count_without_gpu_is_safe():
     assert N.load().cgp_device_count() >= 0
 

@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--tile", type=int, default=4096)
     ap.add_argument("--jitter", type=float, default=0.0)
     ap.add_argument("--spot", type=int, default=16)
+    ap.add_argument("--pred-var", action="store_true",
+                    help="also the posterior variance of the test points (prior diag "
+                         "+ dtrsm on the factor), reported outside total_s")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -157,6 +160,18 @@ def main():
         res.update(solve_s=round(t5 - t4, 2), solve_tflops=round(args.n ** 3 / 3 / (t5 - t4) / 1e12, 2),
                    predict_s=round(t6 - t5, 3), residual=float(r),
                    synthetic_accuracy=acc, total_s=round(t6 - t0, 2))
+        if args.pred_var:
+            with torch.no_grad():
+                t7 = time.perf_counter()
+                kz = model(Z, Z, True, True)             # Kt_diag, save_kernel.py:33-36
+                torch.cuda.synchronize()
+                t8 = time.perf_counter()
+                var = cnn_gp.predictive_variance(K, Kxz, kz, overwrite_kxz=True)
+                torch.cuda.synchronize()
+                t9 = time.perf_counter()
+            res.update(kz_diag_s=round(t8 - t7, 3), pred_var_s=round(t9 - t8, 3),
+                       pred_var_tflops=round(args.n ** 2 * args.m / (t9 - t8) / 1e12, 2),
+                       pred_var_min=float(var.min()), pred_var_max_over_prior=float((var / kz).max()))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
