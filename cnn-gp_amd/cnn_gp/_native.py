@@ -114,6 +114,7 @@ SIGNATURES = {
     "cgp_pred_var_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp]),
     "cgp_net_geometry": (_i32, [_i32] * 7),
     "cgp_net_hs_elems": (_i32, [_i32]),
+    "cgp_net_supertile": (_i32, []),
     "cgp_net_resolution": (_i32, [_i32, _i32]),
     "cgp_net_op_size": (ctypes.c_size_t, []),
     "cgp_net_args_size": (ctypes.c_size_t, []),

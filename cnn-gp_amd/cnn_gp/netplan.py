@@ -507,9 +507,11 @@ class NetPlan:
 
     @staticmethod
     def units(n1: int, n2: int, same: bool) -> int:
-        """Pair units of a tile: 8x8 supertiles (upper triangle when same) x 64."""
-        nbi, nbj = -(-n1 // 8), -(-n2 // 8)
-        return (nbi * (nbi + 1) // 2 if same else nbi * nbj) * 64
+        """Pair units of a tile: st x st supertiles (upper triangle when same) x st²,
+        st = the library's cgp_net_supertile()."""
+        st = N.load().cgp_net_supertile()
+        nbi, nbj = -(-n1 // st), -(-n2 // st)
+        return (nbi * (nbi + 1) // 2 if same else nbi * nbj) * st * st
 
     def prepare(self, x, y, var, n1: int, n2: int, same: bool, flags: int = 0,
                 out: Optional[torch.Tensor] = None):

@@ -1269,6 +1269,8 @@ int cgp_net_resolution(int32_t h, int32_t w) { return res_index(h, w); }
 size_t cgp_net_op_size(void) { return sizeof(cgp_net_op); }
 size_t cgp_net_args_size(void) { return sizeof(cgp_net_args); }
 
+int cgp_net_supertile(void) { return kST; }
+
 int cgp_net_hs_elems(int32_t code) {
     return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;
 }

@@ -290,6 +290,9 @@ int cgp_net_geometry(int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t taps,
                      int32_t stride, int32_t offset);
 /* elements of row-sum scratch the conv of geometry `code` needs (-1: bad code) */
 int cgp_net_hs_elems(int32_t code);
+/* supertile edge of the pair walk: a tile's pairs are numbered in kST×kST blocks (upper
+ * triangle of blocks when same), kST² units each; hosts size unit ranges with it */
+int cgp_net_supertile(void);
 size_t cgp_net_op_size(void);
 size_t cgp_net_args_size(void);
 /* Elementwise-op size code for cgp_net_op.code, or -1 (generic runtime-size path). */
