@@ -21,8 +21,6 @@
 
 #include "cgp_common.h"
 
-#include <atomic>
-#include <mutex>
 
 #include <algorithm>
 #include <climits>
@@ -1128,32 +1126,21 @@ int net_occupancy_for(int lds_bytes, int flags, int np) {
     return fn ? net_occupancy(fn, lds_bytes * np) : 0;
 }
 
-// Per-XCD unit counters for a launch: slots of 8 counters rotate through one device
-// buffer (a slot is reused 64 launches later, long after its launch has drained) and are
-// zeroed on the launch stream.
-unsigned long long* work_counters(void* stream) {
-    constexpr int kSlots = 64, kDevices = 64;
-    static std::mutex mu;
-    static unsigned long long* buf[kDevices] = {};
-    static std::atomic<unsigned> next{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevices) {
+// Per-XCD unit counters for a launch: 8 × u64 from the stream-ordered pool, zeroed on the
+// launch stream and freed behind the kernel on the same stream, so a block is never handed
+// to another launch (on any stream) while this one can still read it.
+unsigned long long* work_counters(hipStream_t s) {
+    void* ctr = nullptr;
+    if (hipMallocAsync(&ctr, sizeof(unsigned long long) * 8, s) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        if (!buf[dev] &&
-            hipMalloc(&buf[dev], sizeof(unsigned long long) * 8 * kSlots) != hipSuccess) {
-            (void)hipGetLastError();
-            buf[dev] = nullptr;
-            return nullptr;
-        }
-    }
-    unsigned long long* slot = buf[dev] + 8 * (next++ % kSlots);
-    if (hipMemsetAsync(slot, 0, sizeof(unsigned long long) * 8, as_stream(stream)) != hipSuccess)
+    if (hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * 8, s) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFreeAsync(ctr, s);
         return nullptr;
-    return slot;
+    }
+    return static_cast<unsigned long long*>(ctr);
 }
 
 template <typename T>
@@ -1170,11 +1157,14 @@ int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, 
     if (grid > groups) grid = groups;
     grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
     NetP<T> arg = p;
-    arg.work = work_counters(stream);
+    hipStream_t s = as_stream(stream);
+    arg.work = work_counters(s);
     if (!arg.work) return fail(CGP_EHIP, "net: work counters");
     void* args[] = {&arg};
-    CGP_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args, (size_t)wg_bytes,
-                            as_stream(stream)));
+    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args,
+                                         (size_t)wg_bytes, s);
+    (void)hipFreeAsync(arg.work, s);           // stream-ordered: after the kernel
+    if (e != hipSuccess) return fail(CGP_EHIP, "net_kernel launch: %s", hipGetErrorString(e));
     return check_launch("net_kernel");
 }
 

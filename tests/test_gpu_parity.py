@@ -550,6 +550,34 @@ def test_predict_and_cast():
     np.testing.assert_array_equal(out.cpu().numpy(), f32[1].astype(np.float64))
 
 
+def test_concurrent_streams_match():
+    """tiles of one Kxx evaluated on two streams at once (about 100 staged launches in
+    flight, each with its own per-XCD work counters) equal the one-launch result"""
+    m = configs_util.model("mnist_as_tf").double().to(DEV)
+    g = torch.Generator().manual_seed(12)
+    X = torch.rand((192, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    with torch.no_grad():
+        ref = m(X)
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = []
+        B = 32
+        for rep in range(2):
+            for a in range(0, 192, B):
+                for b in range(a, 192, B):
+                    st = streams[(a // B + b // B + rep) % 2]
+                    with torch.cuda.stream(st):
+                        outs.append((a, b, m(X[a:a + B], X[b:b + B], a == b, False)))
+        torch.cuda.synchronize()
+    for a, b, k in outs:
+        blk = ref[a:a + B, b:b + B]
+        if a == b:
+            iu = torch.triu_indices(B, B, 1)
+            assert torch.equal(k[iu[0], iu[1]], blk[iu[0], iu[1]])
+        else:
+            assert torch.equal(k, blk)
+
+
 def _joint_spd(n, m, seed):
     rng = np.random.default_rng(seed)
     A = rng.standard_normal((n + m, n + m + 8))
