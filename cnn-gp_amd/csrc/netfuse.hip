@@ -955,17 +955,20 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // flight on an XCD stay one contiguous window (a few supertiles) whose images and
     // variance maps its L2 holds; a static stride lets workgroups drift apart and the
     // window (and L2 misses) grow.  The next group's index is fetched one pair ahead.
-    __shared__ long long next_u;
+    // two slots used alternately: a slot is rewritten two advances later, after every
+    // thread has passed the barrier of the advance in between, so one barrier suffices
+    __shared__ long long next_u[2];
+    int adv = 0;
     unsigned long long* ctr = p.work + xcd;
     (void)g8;
     (void)l;
     unsigned long long grab = 0;   // thread 0: the counter value fetched one pair ahead
     if (tid == 0) grab = atomicAdd(ctr, 1ull);
     auto advance = [&]() {
-        if (tid == 0) next_u = beg + (long long)grab * NP;
+        if (tid == 0) next_u[adv] = beg + (long long)grab * NP;
         lds_barrier();
-        const long long v = next_u;
-        lds_barrier();
+        const long long v = next_u[adv];
+        adv ^= 1;
         return v;
     };
     for (long long u = advance(); u < end; u = advance()) {
