@@ -160,6 +160,66 @@ def probe_kernels(model, x, n1, n2, reps=10):
     return res
 
 
+def conv_stencil_roofline(model, x, B, reps=5):
+    """Conv2d.propagate alone (kernels.py:92-98; no fused ReLU / moments / Sum) — the
+    north star's "Conv2d covariance kernel" — at the config's most frequent conv shape, on
+    the B·B pair maps of one tile, timed with HIP events on the launch stream; against the
+    8 TB/s HBM roof with algorithmic bytes 8·P·(H·W + Ho·Wo).  A torch copy of the same
+    input is timed beside it as the achievable-bandwidth reference."""
+    from collections import Counter
+    _, C, h, w = x.shape
+    plan = model._plan(h, w)
+    convs = Counter((op.geom.taps, op.geom.offset, op.geom.stride, op.shape_in, op.shape_out)
+                    for op in plan.prog.ops
+                    if op.kind == "conv" and op.geom.dilation == 1 and op.shape_out[0] > 1)
+    if not convs:
+        return None
+    (k, off, st, (hi, wi), (ho, wo)), _ = convs.most_common(1)[0]
+    P = B * B
+    g = torch.Generator(device="cpu").manual_seed(0)
+    var = torch.rand((2 * B, hi, wi), generator=g, dtype=x.dtype).add_(0.5).to(x.device)
+    xy = (0.5 * (var[:B, None] * var[None, B:]).sqrt()).reshape(P, hi, wi).contiguous()
+    del var
+    out = torch.empty((P, ho, wo), dtype=x.dtype, device=x.device)
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    a = N.ConvArgs()
+    a.in_, a.out = N.ptr(xy), N.ptr(out)
+    a.nmaps, a.n1, a.n2 = P, B, B
+    a.h, a.w, a.ho, a.wo = hi, wi, ho, wo
+    a.taps, a.offset, a.stride, a.dilation = k, off, st, 1
+    a.weight, a.bias = 1.0 / (k * k), 0.1
+    fn = getattr(N.load(), "cgp_conv_" + ("f64" if x.dtype == torch.float64 else "f32"))
+
+    def timed(launch):
+        launch()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms = timed(lambda: N.check(fn(a, s), "cgp_conv"))
+    cp = torch.empty_like(xy)
+    ms_copy = timed(lambda: cp.copy_(xy))
+    item = x.element_size()
+    nbytes = P * (hi * wi + ho * wo) * item
+    ach = nbytes / (ms * 1e-3) / 1e9
+    copy_gbs = 2 * P * hi * wi * item / (ms_copy * 1e-3) / 1e9
+    del xy, out, cp
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": f"conv{k}s{st}@{hi}->{ho}", "avg_ms": round(ms, 4),
+            "alg_bytes_per_launch": int(nbytes), "maps_per_launch": P,
+            "torch_copy_GBs": round(copy_gbs, 1),
+            "note": "Conv2d.propagate alone on one tile's pair maps (the layer path fuses the "
+                    "ReLU into it; the whole-network kernel replaces both)"}
+
+
 def alg_flops_per_pair(plan):
     """The reference's direct-stencil conv flops per pair: F.conv2d does
     2·extent² flops per output pixel (extent = k, or k + 1 for an even "same" kernel).
@@ -369,6 +429,10 @@ def main():
             roof = layer
         else:
             extra["layer_path_conv_roofline"] = layer
+        with torch.no_grad():
+            stencil = conv_stencil_roofline(model, X[:B], B)
+        if stencil is not None:
+            extra["conv_stencil_roofline"] = stencil
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
