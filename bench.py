@@ -63,11 +63,15 @@ def parse():
 
 
 def blocks_for_world(n1: int, tile: int, world: int) -> int:
-    """Smallest n_blocks whose upper-triangular tile count covers world × the 1-GPU one."""
+    """Smallest n_blocks whose upper-triangular tile count covers world × the 1-GPU one
+    and whose work splits evenly: in half-tile units (a diagonal tile evaluates half the
+    pairs of an off-diagonal one) nb blocks hold nb(nb−1) + nb = nb² units, so nb² must
+    divide by the world size (at 8 ranks 13 blocks would leave one rank 4% over the
+    mean; 16 blocks give every rank exactly 32 units)."""
     b1 = -(-n1 // tile)
     target = b1 * (b1 + 1) // 2 * world
     nb = b1
-    while nb * (nb + 1) // 2 < target:
+    while nb * (nb + 1) // 2 < target or (world > 1 and (nb * nb) % world):
         nb += 1
     return nb
 

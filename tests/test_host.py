@@ -281,6 +281,9 @@ def test_bench_balanced_split_covers_every_tile_once():
         cost = lambda t: B * (B - 1) // 2 if t[0] else B * B  # noqa: E731
         loads = [sum(cost(t) for t in p) for p in parts]
         assert max(loads) - sum(loads) / world <= B * B
+        # nb² divisible by the world size: every rank within a few pairs of the mean
+        assert (nb * nb) % world == 0 or world == 1
+        assert max(loads) <= sum(loads) / world * (1 + 1e-3), (world, loads)
 
 
 # ------------------------------------------------------------------------------------
