@@ -264,6 +264,12 @@ def needed_variances(ops) -> set:
 # ------------------------------------------------------------------------------------
 # execution
 # ------------------------------------------------------------------------------------
+def _adjacent(x, y) -> bool:
+    """y's elements start where x's end (one allocation, x then y), both contiguous."""
+    return (x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype
+            and y.data_ptr() == x.data_ptr() + x.numel() * x.element_size())
+
+
 class Plan:
     """A compiled model at one input geometry: the variance program and the fused pair
     program.  Cached per (H, W, fuse) on the model."""
@@ -318,8 +324,12 @@ class Plan:
                 buf = torch.empty((n1 + n2, ho, wo), dtype=xx0.dtype, device=dev)
                 g = op.geom
                 h, w = op.shape_in
-                # xx and yy may live in different allocations: launch per block
-                for src, dst, n in ((xin, buf[:n1], n1), (yin, buf[n1:], n2)):
+                # xx and yy may live in different allocations: launch per block, or once
+                # over both when they are adjacent (every value after the first is)
+                parts = ((xin, buf[:n1], n1), (yin, buf[n1:], n2))
+                if _adjacent(xin, yin):
+                    parts = ((xin, buf, n1 + n2),)
+                for src, dst, n in parts:
                     a = N.ConvArgs()
                     a.in_, a.out = N.ptr(src), N.ptr(dst)
                     a.nmaps, a.n1, a.n2 = n, n, 1
@@ -337,10 +347,12 @@ class Plan:
             elif op.kind == "add":
                 buf = torch.empty((n1 + n2, ho, wo), dtype=xx0.dtype, device=dev)
                 outx, outy = buf[:n1], buf[n1:]
-                for part, o, n in ((0, outx, n1), (1, outy, n2)):
+                whole = all(_adjacent(*vals[t]) for _, t in op.terms)
+                for part, o, n in (((None, buf, n1 + n2),) if whole else
+                                   ((0, outx, n1), (1, outy, n2))):
                     first = True
                     for coef, t in op.terms:
-                        src = vals[t][part]
+                        src = vals[t][0] if part is None else vals[t][part]
                         if first:
                             alpha = 1.0 if coef is None else coef
                             N.call(f"cgp_axpby_{sfx}", alpha, N.ptr(src), 0.0, None, N.ptr(o),
