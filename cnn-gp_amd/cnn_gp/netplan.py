@@ -570,6 +570,16 @@ class NetPlan:
                     N.check(fn(ctypes.byref(a), stream), "cgp_net")
 
         def launch(stream, keep=keep, states=states):
+            # the op lists were uploaded and the state buffers allocated on torch's current
+            # stream: a launch on another stream first waits for that stream, and the
+            # caching allocator is told the buffers are in use there, so it cannot hand
+            # them out again while the kernels still read them
+            cur = torch.cuda.current_stream(x.device)
+            if stream and stream != cur.cuda_stream:
+                ext = torch.cuda.ExternalStream(stream, device=x.device)
+                ext.wait_stream(cur)
+                for t in keep + [s for s in states if s is not None]:
+                    t.record_stream(ext)
             if TIMING is not None:
                 st_ = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
                 e0 = torch.cuda.Event(enable_timing=True)

@@ -17,6 +17,14 @@ int check_launch(const char* what);
 // compute units of the current device (cached; launch geometry of persistent kernels)
 int device_cus();
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// the device that owns stream s (the current device for the null stream)
+inline hipError_t stream_device(hipStream_t s, int* dev) {
+    if (s == nullptr) return hipGetDevice(dev);
+    hipDevice_t d = 0;
+    const hipError_t e = hipStreamGetDevice(s, &d);
+    if (e == hipSuccess) *dev = (int)d;
+    return e;
+}
 
 #define CGP_HIP(call)                                                                  \
     do {                                                                               \

@@ -1082,23 +1082,48 @@ int axpby_impl(double alpha, const T* a, double beta, const T* b, T* out, int64_
     return check_launch("axpby_kernel");
 }
 
-// rocBLAS handle per device, created on first use and kept for the process lifetime
-std::mutex g_blas_mu;
-std::map<int, rocblas_handle> g_blas;
+// rocBLAS state per device, created on first use and kept for the process lifetime: the
+// handle, the lock that serialises its users (a handle carries one stream), and a device
+// word for potrf's info (no allocation per call).  Callers on different devices never
+// contend: the registry lock is held only for the lookup.
+struct BlasDev {
+    rocblas_handle h = nullptr;
+    std::mutex mu;
+    int64_t* dinfo = nullptr;
+};
+std::mutex g_blas_reg_mu;
+std::map<int, BlasDev*> g_blas;
 
-int blas_handle(rocblas_handle* h) {
+int blas_dev(hipStream_t s, BlasDev** out) {
     int dev = 0;
-    CGP_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(g_blas_mu);
-    auto it = g_blas.find(dev);
-    if (it == g_blas.end()) {
+    CGP_HIP(stream_device(s, &dev));
+    BlasDev* b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_blas_reg_mu);
+        auto it = g_blas.find(dev);
+        if (it == g_blas.end()) it = g_blas.emplace(dev, new BlasDev).first;
+        b = it->second;
+    }
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!b->h) {
+        int cur = 0;
+        CGP_HIP(hipGetDevice(&cur));
+        CGP_HIP(hipSetDevice(dev));
         rocblas_handle nh;
         rocblas_status st = rocblas_create_handle(&nh);
+        hipError_t e = hipSuccess;
+        if (st == rocblas_status_success)
+            e = hipMalloc(reinterpret_cast<void**>(&b->dinfo), sizeof(int64_t));
+        (void)hipSetDevice(cur);
         if (st != rocblas_status_success)
             return fail(CGP_EBLAS, "rocblas_create_handle: %s", rocblas_status_to_string(st));
-        it = g_blas.emplace(dev, nh).first;
+        if (e != hipSuccess) {
+            (void)rocblas_destroy_handle(nh);
+            return fail(CGP_EHIP, "blas: info word: %s", hipGetErrorString(e));
+        }
+        b->h = nh;
     }
-    *h = it->second;
+    *out = b;
     return CGP_OK;
 }
 
@@ -1219,10 +1244,11 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
         return fail(CGP_EINVAL, "chol_solve: bad sizes n=%lld ldk=%lld nrhs=%lld ldb=%lld",
                     (long long)n, (long long)ldk, (long long)nrhs, (long long)ldb);
     hipStream_t s = as_stream(stream);
-    rocblas_handle h;
-    int rc = blas_handle(&h);
+    BlasDev* b = nullptr;
+    int rc = blas_dev(s, &b);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g_blas_mu);
+    std::lock_guard<std::mutex> lk(b->mu);
+    rocblas_handle h = b->h;
     CGP_BLAS(rocblas_set_stream(h, s));
     if (jitter != 0.0) {
         hipLaunchKernelGGL(diag_add_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, k,
@@ -1230,33 +1256,16 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
         rc = check_launch("diag_add_kernel");
         if (rc) return rc;
     }
-    int64_t* dinfo = nullptr;
-    CGP_HIP(hipMallocAsync(reinterpret_cast<void**>(&dinfo), sizeof(int64_t), s));
     // row-major upper triangle == column-major lower triangle
-    rocblas_status st = rocsolver_dpotrf_64(h, rocblas_fill_lower, n, k, ldk, dinfo);
+    CGP_BLAS(rocsolver_dpotrf_64(h, rocblas_fill_lower, n, k, ldk, b->dinfo));
     int64_t hinfo = -1;
-    if (st == rocblas_status_success) {
-        hipError_t e = hipMemcpyAsync(&hinfo, dinfo, sizeof(int64_t), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) {
-            (void)hipFreeAsync(dinfo, s);
-            return fail(CGP_EHIP, "chol_solve: info readback: %s", hipGetErrorString(e));
-        }
-    }
-    if (st != rocblas_status_success) {
-        (void)hipFreeAsync(dinfo, s);
-        return fail(CGP_EBLAS, "rocsolver_dpotrf_64: %s", rocblas_status_to_string(st));
-    }
+    CGP_HIP(hipMemcpyAsync(&hinfo, b->dinfo, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CGP_HIP(hipStreamSynchronize(s));
     *info = hinfo;
     if (hinfo == 0) {
-        st = rocsolver_dpotrs_64(h, rocblas_fill_lower, n, nrhs, k, ldk, bt, ldb);
-        if (st != rocblas_status_success) {
-            (void)hipFreeAsync(dinfo, s);
-            return fail(CGP_EBLAS, "rocsolver_dpotrs_64: %s", rocblas_status_to_string(st));
-        }
+        CGP_BLAS(rocsolver_dpotrs_64(h, rocblas_fill_lower, n, nrhs, k, ldk, bt, ldb));
+        CGP_HIP(hipStreamSynchronize(s));
     }
-    CGP_HIP(hipFreeAsync(dinfo, s));
-    CGP_HIP(hipStreamSynchronize(s));
     return CGP_OK;
 }
 
@@ -1264,10 +1273,11 @@ int cgp_gemm_f64(const double* a, const double* b, double* c, int64_t m, int64_t
                  int64_t kdim, void* stream) {
     if (!a || !b || !c || m <= 0 || n <= 0 || kdim <= 0)
         return fail(CGP_EINVAL, "gemm: bad arguments");
-    rocblas_handle h;
-    int rc = blas_handle(&h);
+    BlasDev* bd = nullptr;
+    int rc = blas_dev(as_stream(stream), &bd);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g_blas_mu);
+    std::lock_guard<std::mutex> lk(bd->mu);
+    rocblas_handle h = bd->h;
     CGP_BLAS(rocblas_set_stream(h, as_stream(stream)));
     const double one = 1.0, zero = 0.0;
     CGP_BLAS(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
@@ -1285,11 +1295,12 @@ int cgp_pred_var_f64(const double* k, int64_t n, int64_t ldk, double* kxz, int64
                     (long long)n, (long long)ldk, (long long)m, (long long)ldz);
     if (m == 0) return CGP_OK;
     hipStream_t s = as_stream(stream);
-    rocblas_handle h;
-    int rc = blas_handle(&h);
+    BlasDev* bd = nullptr;
+    int rc = blas_dev(s, &bd);
     if (rc) return rc;
     {
-        std::lock_guard<std::mutex> lk(g_blas_mu);
+        std::lock_guard<std::mutex> lk(bd->mu);
+        rocblas_handle h = bd->h;
         CGP_BLAS(rocblas_set_stream(h, s));
         CGP_BLAS(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
         const double one = 1.0;

@@ -1133,10 +1133,13 @@ int net_occupancy_for(int lds_bytes, int flags, int np) {
 }
 
 // Per-XCD unit counters for a launch: 8 × u64 slots of a 64-slot ring owned by the launch
-// stream (one ring per device and stream), zeroed on that stream.  A slot is reused only
-// by a later launch on the same stream, i.e. after this one has drained; launches on
-// other streams never see it.  (Per-launch hipMallocAsync/hipFreeAsync was measured 5%
-// slower on mnist_as_tf: the pool operations open gaps between back-to-back kernels.)
+// stream (one ring per (device, stream), allocated on the device that owns the stream),
+// zeroed on that stream.  A slot is reused only by a later launch on the same stream, i.e.
+// after this one has drained; launches on other streams never see it.  A ring lives as
+// long as the process (a stream destroyed and re-created at the same address reuses its
+// ring, which is safe: the old stream's launches have drained by then).  (Per-launch
+// hipMallocAsync/hipFreeAsync was measured 5% slower on mnist_as_tf: the pool operations
+// open gaps between back-to-back kernels.)
 unsigned long long* work_counters(hipStream_t s) {
     constexpr int kSlots = 64;
     struct Ring {
@@ -1146,7 +1149,7 @@ unsigned long long* work_counters(hipStream_t s) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, Ring> rings;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) {
+    if (stream_device(s, &dev) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
@@ -1154,11 +1157,18 @@ unsigned long long* work_counters(hipStream_t s) {
     {
         std::lock_guard<std::mutex> lock(mu);
         Ring& r = rings[{dev, s}];
-        if (!r.buf &&
-            hipMalloc(&r.buf, sizeof(unsigned long long) * 8 * kSlots) != hipSuccess) {
-            (void)hipGetLastError();
-            r.buf = nullptr;
-            return nullptr;
+        if (!r.buf) {
+            int cur = 0;
+            hipError_t e = hipGetDevice(&cur);
+            if (e == hipSuccess && cur != dev) e = hipSetDevice(dev);
+            if (e == hipSuccess)
+                e = hipMalloc(&r.buf, sizeof(unsigned long long) * 8 * kSlots);
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                r.buf = nullptr;
+                return nullptr;
+            }
         }
         slot = r.buf + 8 * (r.next++ % kSlots);
     }

@@ -163,10 +163,14 @@ def _axpby(terms, kp0):
     return make_kp(kp0["same"], kp0["diag"], xy, xx, yy)
 
 
-def softmax_f32(logits, weights: str):
-    lg = np.asarray(logits, dtype=np.float32 if weights == "f32" else np.float64)
+def softmax(logits, weights: str, dt):
+    """F.softmax(self.logit, dim=0) of Mixture.propagate (kernels.py:221).  The logit
+    Parameter is created in torch's default dtype (float32 under weights="f32") and cast
+    with the model (``.double()``), so the softmax runs in the model's dtype on the
+    float32-rounded logits.  ATen's CPU softmax scales exp(x - max) by 1/Σ."""
+    lg = np.asarray(logits, dtype=np.float32 if weights == "f32" else np.float64).astype(dt)
     e = np.exp(lg - lg.max())
-    return e / e.sum()
+    return e * (dt(1) / e.sum())
 
 
 def propagate(spec, kp: dict, weights: str = "f32") -> dict:
@@ -183,8 +187,8 @@ def propagate(spec, kp: dict, weights: str = "f32") -> dict:
         outs = [propagate(m, kp, weights) for m in spec[1]]
         return _axpby([(None, o) for o in outs], kp)
     if kind == "mix":                                  # kernels.py:220-225
-        pr = softmax_f32(spec[2], weights)
         dt = kp["xy"].dtype.type
+        pr = softmax(spec[2], weights, dt)
         outs = [propagate(m, kp, weights) for m in spec[1]]
         return _axpby([(dt(pr[i]), o) for i, o in enumerate(outs)], kp)
     raise ValueError(f"unknown spec kind {kind!r}")

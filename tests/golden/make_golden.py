@@ -18,6 +18,8 @@ Fixtures (all inputs are float32-representable, stored as float32):
                   model(X[:6], Z, same=False, diag=True) for every config, fp64 and fp32
   tiles.npz       save_K tile assembly with a fake h5 file (NaN pattern, worker split)
   solve.npz       scipy posv on a reference Kxx with NaN lower triangle
+  e2e_mixture.npz Mixture (3 branches, non-zero logits) + 3-term Sum networks at 28x28
+                  (whole-network kernel shapes) and 10x10 (layer path), fp64 and fp32
 """
 from __future__ import annotations
 
@@ -259,9 +261,49 @@ def gen_solve():
     cfg.initial_model.to(torch.float32)
 
 
+def mixture_nets(m):
+    """The two Mixture networks of e2e_mixture.npz, built from module namespace ``m``
+    (the reference's cnn_gp here; tests/test_gpu_parity.py builds the same ones from the
+    build's package).  Logits are non-zero so every softmax weight differs."""
+    logit = torch.tensor([0.3, -0.2, 0.1])
+    big = m.Sequential(
+        m.Conv2d(3, var_bias=0.3),
+        m.Mixture([m.Sequential(),
+                   m.Sequential(m.ReLU(), m.Conv2d(3, var_weight=2.0)),
+                   m.Sequential(m.ReLU(), m.Conv2d(7))], logit.clone()),
+        m.Sum([m.Sequential(), m.ReLU(),
+               m.Sequential(m.ReLU(), m.Conv2d(1, var_bias=0.5))]),
+        m.ReLU(), m.Conv2d(28, padding=0))
+    small = m.Sequential(
+        m.Conv2d(3, var_bias=0.3),
+        m.Mixture([m.Sequential(),
+                   m.Sequential(m.ReLU(), m.Conv2d(3, var_weight=2.0)),
+                   m.Sequential(m.ReLU(), m.Conv2d(5))], torch.tensor([1.1, -0.7, 0.25])),
+        m.ReLU(), m.Conv2d(10, padding=0))
+    return {"big": (big, 28), "small": (small, 10)}
+
+
+def gen_mixture():
+    recs = {}
+    rng = np.random.default_rng(77)
+    for name, (model, side) in mixture_nets(cnn_gp).items():
+        X = uniform(7, 1, side, rng)
+        Z = mnist_like(5, 1, side, rng) if side == 28 else uniform(5, 1, side, rng)
+        recs[f"{name}_X"], recs[f"{name}_Z"] = X, Z
+        for dtn, tdt in (("f64", torch.float64), ("f32", torch.float32)):
+            mod = model.to(tdt)
+            Xt, Zt = torch.from_numpy(X).to(tdt), torch.from_numpy(Z).to(tdt)
+            with torch.no_grad():
+                recs[f"{name}_{dtn}_Kxx"] = mod(Xt).numpy()
+                recs[f"{name}_{dtn}_Kxz"] = mod(Xt, Zt, False, False).numpy()
+                recs[f"{name}_{dtn}_Kxdiag"] = mod(Xt, Xt, True, True).numpy()
+    np.savez_compressed(os.path.join(OUT, "e2e_mixture.npz"), **recs)
+    print("mixture:", len(recs), "arrays")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["conv", "relu", "e2e", "tiles", "solve"]
+    which = sys.argv[1:] or ["conv", "relu", "e2e", "tiles", "solve", "mixture"]
     for w in which:
         {"conv": gen_conv_ops, "relu": gen_relu_ops, "e2e": gen_e2e, "tiles": gen_tiles,
-         "solve": gen_solve}[w]()
+         "solve": gen_solve, "mixture": gen_mixture}[w]()

@@ -417,27 +417,29 @@ def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, monkeypatch):
     assert rel_err(a, ref) < RTOL64["fast"]
 
 
-def test_netfuse_mixture_and_multiterm_sum():
-    """LINEAR ops: a 3-branch Mixture and a 3-term Sum at 28x28 (fused geometries)"""
-    spec_m = cnn_gp.Sequential(
-        cnn_gp.Conv2d(3, var_bias=0.3),
-        cnn_gp.Mixture([cnn_gp.Sequential(),
-                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3, var_weight=2.0)),
-                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(7))],
-                       torch.tensor([0.3, -0.2, 0.1])),
-        cnn_gp.Sum([cnn_gp.Sequential(), cnn_gp.ReLU(),
-                    cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(1, var_bias=0.5))]),
-        cnn_gp.ReLU(), cnn_gp.Conv2d(28, padding=0))
-    rng = np.random.default_rng(8)
-    X = rng.random((5, 1, 28, 28))
-    Z = rng.random((3, 1, 28, 28))
-    m = spec_m.double().to(DEV)
-    assert _uses_net(m, 28, 8)
-    ref = O.kernel(configs_util.spec_of(spec_m), X, Z, False, False)
-    got = m(dev(X), dev(Z), False, False).cpu().numpy()
-    assert rel_err(got, ref) < 1e-6     # softmax: torch (product) vs numpy (oracle)
-    lay = m.set_fused_network(False)(dev(X), dev(Z), False, False).cpu().numpy()
-    assert rel_err(got, lay) < 1e-12
+@pytest.mark.parametrize("net", ["big", "small"])
+@pytest.mark.parametrize("dtn", ["f64", "f32"])
+@pytest.mark.parametrize("numerics", NUMERICS)
+def test_mixture_matches_reference_golden(net, dtn, numerics):
+    """Mixture with non-zero logits (kernels.py:220-225) + a 3-term Sum against the
+    reference's own outputs (tests/golden/e2e_mixture.npz): "big" runs in the
+    whole-network kernel (LINEAR ops at 28x28), "small" (10x10) on the layer path"""
+    z = load("e2e_mixture.npz")
+    model, side = configs_util.mixture_nets()[net]
+    tdt = torch.float64 if dtn == "f64" else torch.float32
+    m = model.to(DEV, tdt).set_exact_relu(numerics == "exact")
+    assert _uses_net(m, side, 8) == (net == "big")
+    X, Z = dev(z[net + "_X"], tdt), dev(z[net + "_Z"], tdt)
+    tol = RTOL64[numerics] if dtn == "f64" else RTOL32
+    with torch.no_grad():
+        got = {"Kxx": m(X), "Kxz": m(X, Z, False, False), "Kxdiag": m(X, X, True, True)}
+        for name, t in got.items():
+            err = rel_err(t.cpu().numpy(), z[f"{net}_{dtn}_{name}"])
+            assert err < tol, (net, dtn, numerics, name, err)
+        if net == "big":      # the layer path evaluates the same LINEAR ops
+            lay = m.set_fused_network(False)(X, Z, False, False)
+            assert rel_err(got["Kxz"].cpu().numpy(), lay.cpu().numpy()) < \
+                (1e-12 if dtn == "f64" else RTOL32)
 
 
 def test_cpu_inputs_round_trip_to_host():
@@ -447,22 +449,6 @@ def test_cpu_inputs_round_trip_to_host():
     K = m(X)
     assert K.device.type == "cpu"
     assert rel_err(K.numpy(), z["s0_mnist_f64_Kxx"]) < RTOL64["fast"]
-
-
-def test_mixture_against_oracle():
-    spec_m = cnn_gp.Sequential(
-        cnn_gp.Conv2d(3, var_bias=0.3),
-        cnn_gp.Mixture([cnn_gp.Sequential(),
-                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(3, var_weight=2.0)),
-                        cnn_gp.Sequential(cnn_gp.ReLU(), cnn_gp.Conv2d(5))],
-                       torch.tensor([0.3, -0.2, 0.1])),
-        cnn_gp.ReLU(), cnn_gp.Conv2d(10, padding=0))
-    rng = np.random.default_rng(8)
-    X = rng.random((4, 1, 10, 10))
-    Z = rng.random((3, 1, 10, 10))
-    ref = O.kernel(configs_util.spec_of(spec_m), X, Z, False, False)
-    got = spec_m.double().to(DEV)(dev(X), dev(Z), False, False).cpu().numpy()
-    assert rel_err(got, ref) < 1e-6     # softmax: torch (product) vs numpy (oracle)
 
 
 # ------------------------------------------------------------------------------------
@@ -535,8 +521,24 @@ def test_solve_golden_nan_lower():
 
 def test_solve_not_pd_raises():
     K = torch.tensor([[1.0, 2.0], [2.0, 1.0]], dtype=torch.float64, device=DEV)
+    keep = K.clone()
     with pytest.raises(np.linalg.LinAlgError):
         cnn_gp.solve_system(K, torch.ones(2, 1, dtype=torch.float64, device=DEV))
+    assert torch.equal(K, keep)          # default: the caller's Kxx is never modified
+
+
+def test_solve_leaves_kxx_by_default_and_factors_in_place_on_request():
+    z = load("solve.npz")
+    K = torch.from_numpy(z["K"].copy()).to(DEV)
+    Y = torch.from_numpy(z["Y"]).to(DEV)
+    keep = K.clone()
+    a = cnn_gp.solve_system(K, Y, jitter=float(z["jitter"]))
+    assert torch.equal(K, keep)
+    b = cnn_gp.solve_system(K, Y, jitter=float(z["jitter"]), overwrite_a=True)
+    assert torch.equal(a, b)
+    U = torch.triu(K).cpu().numpy()      # the row-major upper triangle holds U, K = UᵀU
+    A = z["K"] + float(z["jitter"]) * np.eye(len(U))
+    np.testing.assert_allclose(U.T @ U, A, rtol=1e-10, atol=1e-10 * np.abs(A).max())
 
 
 def test_predict_and_cast():
@@ -598,7 +600,7 @@ def test_predictive_variance_vs_numpy(n, m):
     K[tuple(np.tril_indices(n, -1))] = float("nan")
     K = K.to(DEV)
     Y = torch.ones((n, 1), dtype=torch.float64, device=DEV)
-    cnn_gp.solve_system(K, Y)                      # K now holds the factor
+    cnn_gp.solve_system(K, Y, overwrite_a=True)    # K now holds the factor
     Kxz = dev(J[n:, :n])
     keep = Kxz.clone()
     var = cnn_gp.predictive_variance(K, Kxz, dev(np.diag(J[n:, n:]).copy()))
@@ -631,7 +633,7 @@ def test_predictive_variance_nngp():
     Kxx_h, Kzx_h, kz_h = (t.cpu().numpy() for t in (Kxx, Kzx, kz))
     jitter = 1e-6 * float(np.mean(np.diag(Kxx_h)))
     cnn_gp.solve_system(Kxx, torch.ones((96, 1), dtype=torch.float64, device=DEV),
-                        jitter=jitter)
+                        jitter=jitter, overwrite_a=True)
     var = cnn_gp.predictive_variance(Kxx, Kzx, kz).cpu().numpy()
     A = Kxx_h + jitter * np.eye(96)
     ref = kz_h - np.einsum("tr,rt->t", Kzx_h, np.linalg.solve(A, Kzx_h.T))

@@ -86,6 +86,24 @@ def test_e2e_match_reference(cfg):
                                            err_msg=f"{cfg} {pre} {dtn} {name}")
 
 
+@pytest.mark.parametrize("net", ["big", "small"])
+def test_mixture_matches_reference(net):
+    """Mixture (kernels.py:220-225): softmax of the float32-created logit in the model's
+    dtype, branch-weighted sum; 3-term Sum alongside"""
+    import configs_util
+    z = load("e2e_mixture.npz")
+    model, _ = configs_util.mixture_nets()[net]
+    spec = configs_util.spec_of(model)
+    X, Z = z[net + "_X"], z[net + "_Z"]
+    for dtn, dt, tol in (("f64", np.float64, 1e-11), ("f32", np.float32, 2e-5)):
+        Xd, Zd = X.astype(dt), Z.astype(dt)
+        cases = {"Kxx": O.kernel(spec, Xd), "Kxz": O.kernel(spec, Xd, Zd, False, False),
+                 "Kxdiag": O.kernel(spec, Xd, Xd, True, True)}
+        for name, got in cases.items():
+            np.testing.assert_allclose(got, z[f"{net}_{dtn}_{name}"], rtol=tol, atol=0,
+                                       err_msg=f"{net} {dtn} {name}")
+
+
 def test_tile_schedule_matches_reference():
     z = load("tiles.npz")
     X, Z = z["X"].astype(np.float64), z["Z"].astype(np.float64)

@@ -148,7 +148,7 @@ def main():
         Y = cnn_gp.one_hot_pm1(ytr, 10).to(dev)
         torch.cuda.synchronize()
         t4 = time.perf_counter()
-        A = cnn_gp.solve_system(K, Y, jitter=args.jitter)     # K overwritten by its factor
+        A = cnn_gp.solve_system(K, Y, jitter=args.jitter, overwrite_a=True)   # K -> factor
         torch.cuda.synchronize()
         t5 = time.perf_counter()
         diag_j = torch.arange(len(rows), device=dev)
