@@ -1,24 +1,39 @@
 """Benchmark: NNGP Gram-matrix build (kernel entries/s) + GP solve on MI355X.
 
 Workload (BASELINE.json configs[1]): mnist_paper_convnet_gp, Kxx of N = 4096 synthetic
-28×28×1 images, float64, Gram tiles of B = 1024 (the reference's tile schedule:
-upper-triangular tiles, diagonal tiles evaluated in full).  One STEP = every Gram tile of
-this rank evaluated into a device-resident Kxx.
+28×28×1 images, float64, Gram tiles of B = 1024 in the reference's schedule (upper
+triangular tiles).  One STEP = every Gram tile of this rank evaluated into a
+device-resident Kxx.
 
     python bench.py [--gpus N --steps K --warmup W] [--config C --n N --tile B]
 
-Multi-GPU (one process per GPU, torchrun): the Gram tiles of a Kxx whose size grows with
-the world (n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world) are split across ranks by
-evaluated pairs (balanced_split: a diagonal tile costs half) — no data-path collective;
-per-rank work is ~constant ("scaling": "weak").  cnn_gp.gram keeps the reference's
-contiguous split (cnn_gp/data.py:11-19) for HDF5-compatible worker files.
+value = kernel entries the device EVALUATES per second, whole job: B1·B2 for an
+off-diagonal tile, B(B−1)/2 for a diagonal tile (the kernel computes i < j there and
+mirrors; K[i, i] comes from the per-image variance chain).  The reference's schedule
+would count B² for a diagonal tile; that figure is reported as
+``reference_schedule_pairs_per_s`` beside it.
 
-value = evaluated pairs (Σ over all tiles of B1·B2) per second, whole job.  Also
-reported: unique Kxx entries/s, the single-GPU build+solve wall-clock (rocSOLVER
-dpotrf+dpotrs on the assembled Kxx, NaN lower triangle), the dominant kernel's
-roofline fraction measured live with HIP events (the whole-network kernel: fp64 compute
-roof; the layer path: HBM roof), and the CPU oracle's rate on a bounded
-sample of the same workload (cpu_baseline).
+Also on the same JSON line:
+  roofline           the whole-network kernel (net_kernel, fp64 VALU-bound): credited
+                     direct-stencil flops vs the fp64 peak, plus the VALU issue
+                     utilisation and HBM traffic per launch from the committed PMC
+                     passes (profiles/r2/net_pmc.json, rocprofv3)
+  mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
+  solve              rocSOLVER dpotrf_64 + dpotrs_64 on the assembled 4096² Kxx
+  fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
+                     + solve + predict, row-sharded over the ranks with one RCCL gather
+                     per matrix to rank 0 (tools/fullscale.py)
+  conv_stencil_roofline  Conv2d.propagate alone (the north star's "Conv2d covariance
+                     kernel") against the 8 TB/s HBM roof, PMC traffic committed
+  cpu_baseline       the torch-CPU restatement of the reference (oracle/torch_cpu.py,
+                     bit-identical to the reference at C1) on the host threads torch
+                     is given, with the committed calibration against the reference
+
+Multi-GPU (one process per GPU, torchrun): the Kxx grows with the world
+(n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world, work divisible evenly) and its tiles
+are split over the ranks by evaluated pairs — no data-path collective; per-rank work is
+~constant ("scaling": "weak").  The full-scale leg shards its fixed problem ("strong")
+and gathers once per matrix.
 """
 from __future__ import annotations
 
@@ -30,9 +45,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT]
+sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT, os.path.join(ROOT, "tools")]
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -42,7 +56,10 @@ from cnn_gp.data import tile_schedule  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
 FP64_PEAK_TFLOPS = 78.6        # MI355X spec FP64 (vector = matrix); half the FP32 157.3
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "net_traffic.json")
+SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
+CLOCK_HZ = 2.4e9               # peak engine clock
+PMC_FILE = os.path.join(ROOT, "profiles", "r2", "net_pmc.json")
+CALIB_FILE = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
 
 
 def parse():
@@ -57,8 +74,12 @@ def parse():
     p.add_argument("--no-solve", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-probe", action="store_true")
-    p.add_argument("--cpu-pairs", type=int, default=16384,
-                   help="pairs in the CPU-oracle sample (128x128 tile = 16384, ~10-30 s)")
+    p.add_argument("--no-second", action="store_true", help="skip the mnist_as_tf leg")
+    p.add_argument("--no-fullscale", action="store_true")
+    p.add_argument("--fullscale-n", type=int, default=60000)
+    p.add_argument("--fullscale-m", type=int, default=10000)
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
+                   help="target duration of the CPU-baseline sample")
     return p.parse_args()
 
 
@@ -76,92 +97,44 @@ def blocks_for_world(n1: int, tile: int, world: int) -> int:
     return nb
 
 
+def tile_eval_pairs(t, B, n):
+    """pairs the device evaluates for tile (same, bi, bj): i < j on a diagonal tile"""
+    same, i, j = t
+    a, b = min(B, n - i * B), min(B, n - j * B)
+    return a * (a - 1) // 2 if same else a * b
+
+
 def balanced_split(all_tiles, B, n, world):
-    """Per-rank tile lists with equal work: the kernel evaluates a diagonal tile's i < j
-    pairs only (half an off-diagonal tile), so the reference's contiguous split by tile
-    count (cnn_gp/data.py:11-19) would leave the ranks holding fewer diagonal tiles
-    behind.  Longest-processing-time greedy on the pairs each tile evaluates, in the
-    reference's tile order within a rank."""
-    def cost(t):
-        same, i, j = t
-        a, b = min(B, n - i * B), min(B, n - j * B)
-        return a * (a - 1) // 2 if same else a * b
+    """Per-rank tile lists with equal evaluated pairs: longest-processing-time greedy on
+    the pairs each tile evaluates (a diagonal tile costs half), in the reference's tile
+    order within a rank."""
     load = [0] * world
     parts = [[] for _ in range(world)]
-    for k in sorted(range(len(all_tiles)), key=lambda k: -cost(all_tiles[k])):
+    for k in sorted(range(len(all_tiles)), key=lambda k: -tile_eval_pairs(all_tiles[k], B, n)):
         r = min(range(world), key=lambda r: load[r])
-        load[r] += cost(all_tiles[k])
+        load[r] += tile_eval_pairs(all_tiles[k], B, n)
         parts[r].append(k)
     return [[all_tiles[k] for k in sorted(p)] for p in parts]
 
 
-def op_bytes(op, nmaps, n1, n2, C, item):
-    """Algorithmic HBM bytes of one pair-pipeline launch."""
-    h, w = op.shape_in
-    ho, wo = op.shape_out
-    if op.kind == "conv":
-        rd = (n1 + n2) * C * h * w if op.pre == N.CGP_PRE_MOMENTS else nmaps * h * w
-        b = rd + nmaps * ho * wo
-        if op.addend is not None:
-            b += nmaps * ho * wo
-        if op.pre == N.CGP_PRE_RELU:
-            b += (n1 + n2) * h * w
-        if op.post == N.CGP_POST_RELU:
-            b += (n1 + n2) * ho * wo
-    elif op.kind == "relu":
-        b = 2 * nmaps * ho * wo + (n1 + n2) * ho * wo + (nmaps * ho * wo if op.addend else 0)
-    else:
-        b = (2 * len(op.terms)) * nmaps * ho * wo
-    return b * item
-
-
-def op_name(op):
-    if op.kind == "conv":
-        pre = {0: "", 1: "relu+", 2: "moments+"}[op.pre]
-        post = "+relu" if op.post else ""
-        add = "+add" if op.addend is not None else ""
-        return (f"{pre}conv{op.geom.taps}s{op.geom.stride}{post}{add}"
-                f"@{op.shape_in[0]}->{op.shape_out[0]}")
-    return f"{op.kind}@{op.shape_out[0]}"
-
-
-def probe_kernels(model, x, n1, n2, reps=10):
-    """Time every launch of one full tile's pair program with HIP events on the stream the
-    kernels run on; return per-op (name, avg_ms, alg_bytes)."""
-    from cnn_gp.program import Plan
-    stream = torch.cuda.current_stream()
-    s = stream.cuda_stream
-    _, C, h, w = x.shape
-    plan = model._plan(h, w)
-    sfx = Plan._sfx(x.dtype)
-    lib = N.load()
-    var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
-    N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(x), n1, n2, C, h * w,
-                                                    N.ptr(var0[:n1]), N.ptr(var0[n1:]), s), "mv")
-    var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, False, s)
-    xy0 = None
-    if not plan.moments_fused:
-        xy0 = torch.empty((n1 * n2, h, w), dtype=x.dtype, device=x.device)
-        N.check(getattr(lib, f"cgp_moments_xy_{sfx}")(N.ptr(x), N.ptr(x), n1, n2, C, h * w, 0,
-                                                       N.ptr(xy0), s), "mxy")
-    res = []
-    item = x.element_size()
-
-    def probe(idx, op, launch):
+def timed_events(stream, launch, reps):
+    launch()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
         launch()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            launch()
-        e1.record(stream)
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        res.append((op_name(op), ms, op_bytes(op, n1 * n2, n1, n2, C, item)))
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
 
-    plan.run_pairs(x, x, xy0, var, n1, n2, False, False, s, probe=probe)
-    torch.cuda.synchronize()
-    return res
+
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def conv_stencil_roofline(model, x, B, reps=5):
@@ -169,7 +142,8 @@ def conv_stencil_roofline(model, x, B, reps=5):
     north star's "Conv2d covariance kernel" — at the config's most frequent conv shape, on
     the B·B pair maps of one tile, timed with HIP events on the launch stream; against the
     8 TB/s HBM roof with algorithmic bytes 8·P·(H·W + Ho·Wo).  A torch copy of the same
-    input is timed beside it as the achievable-bandwidth reference."""
+    input is timed beside it as the achievable-bandwidth reference.  ``traffic``: the
+    committed PMC pass over the same launch (profiles/r2/net_pmc.json "conv_stencil")."""
     from collections import Counter
     _, C, h, w = x.shape
     plan = model._plan(h, w)
@@ -194,34 +168,28 @@ def conv_stencil_roofline(model, x, B, reps=5):
     a.taps, a.offset, a.stride, a.dilation = k, off, st, 1
     a.weight, a.bias = 1.0 / (k * k), 0.1
     fn = getattr(N.load(), "cgp_conv_" + ("f64" if x.dtype == torch.float64 else "f32"))
-
-    def timed(launch):
-        launch()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            launch()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps
-
-    ms = timed(lambda: N.check(fn(a, s), "cgp_conv"))
+    ms = timed_events(stream, lambda: N.check(fn(a, s), "cgp_conv"), reps)
     cp = torch.empty_like(xy)
-    ms_copy = timed(lambda: cp.copy_(xy))
+    ms_copy = timed_events(stream, lambda: cp.copy_(xy), reps)
     item = x.element_size()
     nbytes = P * (hi * wi + ho * wo) * item
     ach = nbytes / (ms * 1e-3) / 1e9
     copy_gbs = 2 * P * hi * wi * item / (ms_copy * 1e-3) / 1e9
     del xy, out, cp
     torch.cuda.empty_cache()
+    kname = f"conv{k}s{st}@{hi}->{ho}"
+    traffic, pmc_ms = None, None
+    pmc = (load_json(PMC_FILE) or {}).get("conv_stencil")
+    if pmc and pmc.get("kernel") == kname and pmc.get("maps") == P:
+        traffic, pmc_ms = int(pmc["hbm_bytes_per_launch"]), pmc.get("avg_ms")
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": f"conv{k}s{st}@{hi}->{ho}", "avg_ms": round(ms, 4),
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": kname, "avg_ms": round(ms, 4), "pmc_avg_ms": pmc_ms,
             "alg_bytes_per_launch": int(nbytes), "maps_per_launch": P,
             "torch_copy_GBs": round(copy_gbs, 1),
-            "note": "Conv2d.propagate alone on one tile's pair maps (the layer path fuses the "
-                    "ReLU into it; the whole-network kernel replaces both)"}
+            "note": "Conv2d.propagate alone on one tile's pair maps (cgp_conv, no fused "
+                    "epilogue); traffic = 2·FETCH_SIZE + WRITE_SIZE (gfx950 correction) "
+                    "from the committed rocprofv3 pass"}
 
 
 def alg_flops_per_pair(plan):
@@ -255,7 +223,15 @@ def alg_flops_pointwise_per_pair(plan):
 
 def net_roofline(model, x, cfg_name, timing):
     """Roofline of the whole-network kernel from the HIP events recorded around each of its
-    launches in the timed region (cnn_gp.netplan.TIMING, on the launch stream)."""
+    launches in the timed region (cnn_gp.netplan.TIMING, on the launch stream).
+
+    The kernel is fp64-VALU bound ("valu_f64"): per pair it reads two images and L2-resident
+    variance maps and writes one entry, everything else stays in LDS.  ``achieved`` credits
+    the reference's direct-stencil conv flops (the kernel executes fewer: separable window
+    sums), so ``frac`` is a credited figure; ``valu_issue_frac`` is the hardware meter —
+    the fraction of SIMD cycles issuing a VALU instruction (SQ_ACTIVE_INST_VALU, in
+    quad-cycles, × 4 / (1024 SIMDs × clock × kernel time)), from the committed PMC pass
+    scaled per pair to this run's launches."""
     n, C, h, w = x.shape
     plan = model._plan(h, w)
     net = model._net_plan(plan, x.element_size())
@@ -267,51 +243,141 @@ def net_roofline(model, x, cfg_name, timing):
     achieved = fl * pairs / (ms * 1e-3) / 1e12
     fl_pw = fl + alg_flops_pointwise_per_pair(plan)
     achieved_pw = fl_pw * pairs / (ms * 1e-3) / 1e12
-    traffic = None
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f).get(cfg_name)
-        if t and t.get("dtype") == str(x.dtype):
-            # measured on one full tile: scale to this run's average launch
-            traffic = int(t["hbm_bytes_per_launch"] / t["tile"] ** 2 * pairs / len(timing))
-    except (OSError, ValueError):
-        pass
+    per_launch = pairs / len(timing)
+    avg_s = ms * 1e-3 / len(timing)
+    traffic = valu = valu_insts = None
+    pmc_note = "no committed PMC pass for this config/dtype"
+    pmc = (load_json(PMC_FILE) or {}).get(cfg_name)
+    if pmc and pmc.get("dtype") == str(x.dtype):
+        traffic = int(pmc["hbm_bytes_per_pair"] * per_launch)
+        quad = pmc["valu_active_quadcycles_per_pair"] * per_launch
+        valu = round(4 * quad / (SIMDS * CLOCK_HZ * avg_s), 4)
+        valu_insts = round(pmc["valu_insts_per_pair"], 1)
+        pmc_note = (f"PMC: {pmc['source']}; per pair: {pmc['hbm_bytes_per_pair']:.0f} HBM "
+                    f"bytes, {pmc['valu_insts_per_pair']:.0f} VALU wave-instructions")
     kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": traffic,
+    return {"bound": "valu_f64", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
+            "traffic": traffic, "valu_issue_frac": valu,
             "kernel": kname, "launches": len(timing), "avg_ms": round(ms / len(timing), 4),
-            "pairs_per_launch": pairs // len(timing), "alg_flops_per_pair": fl,
-            "alg_flops_per_launch": fl * pairs // len(timing),
+            "pairs_per_launch": int(per_launch), "alg_flops_per_pair": fl,
+            "alg_flops_per_launch": int(fl * per_launch),
             "alg_flops_incl_pointwise_per_pair": fl_pw,
             "achieved_incl_pointwise": round(achieved_pw, 2),
             "frac_incl_pointwise": round(achieved_pw / FP64_PEAK_TFLOPS, 4),
+            "valu_insts_per_pair": valu_insts,
             "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
             "stages": [{"pairs_per_workgroup": st.pairs, "ops": st.n_ops} for st in net.stages],
-            "note": "fp64 compute roof (VALU = MFMA = 78.6 TF on MI355X); algorithmic "
-                    "flops = the reference's direct-stencil conv flops of the pairs the "
-                    "kernel evaluates (same tiles: i < j); one launch = one tile (all its "
-                    "stage kernels); traffic: PMC FETCH/WRITE per tile "
-                    "(profiles/r1/net_traffic.json), scaled to this launch size"}
+            "note": "bound valu_f64: the kernel keeps every map in LDS (HBM carries images, "
+                    "L2-resident variance maps and one entry per pair); peak = fp64 VALU "
+                    "(= fp64 MFMA) 78.6 TF; achieved = credited direct-stencil conv flops of "
+                    "the pairs evaluated (i < j on diagonal tiles); one launch = one tile "
+                    "(all its stage kernels). " + pmc_note}
 
 
-def cpu_baseline(cfg_name, dtype, pairs):
-    """The CPU oracle (numpy restatement, 1 thread) on a bounded sample: one Kxz tile."""
-    from oracle import nngp_oracle as O
-    from oracle import specs
-    side = int(round(pairs ** 0.5))
+def cpu_info():
+    model = "?"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline(cfg_name, dtype, seconds):
+    """The torch-CPU restatement of the reference (oracle/torch_cpu.py — the reference's
+    op sequence, bit-identical to it at C1) on the host threads torch is given, on a Kxz
+    tile sized for about ``seconds`` of work after a small warm-up that measures the
+    rate.  The calibration restatement/reference measured in the build container
+    (tools/calibrate_cpu.py) is quoted beside it."""
+    from oracle import specs, torch_cpu
     spec = specs.CONFIGS[cfg_name]()
     C, hw = specs.GEOMETRY[cfg_name]
-    rng = np.random.default_rng(0)
-    dt = np.float64 if dtype == torch.float64 else np.float32
-    X = rng.random((side, C, hw, hw)).astype(dt)
-    Z = rng.random((side, C, hw, hw)).astype(dt)
+    g = torch.Generator().manual_seed(0)
+    dt = dtype
+    w = torch.rand((32, C, hw, hw), generator=g, dtype=dt)
+    for _ in range(2):                  # the second run measures the warm rate
+        t0 = time.perf_counter()
+        torch_cpu.kernel(spec, w, w.flip(0), False, False)
+        rate = 32 * 32 / (time.perf_counter() - t0)
+    side = int(min(256, max(64, (rate * seconds) ** 0.5)))
+    X = torch.rand((side, C, hw, hw), generator=g, dtype=dt)
+    Z = torch.rand((side, C, hw, hw), generator=g, dtype=dt)
     t0 = time.perf_counter()
-    O.kernel(spec, X, Z, False, False)
+    torch_cpu.kernel(spec, X, Z, False, False)
     el = time.perf_counter() - t0
-    return dict(value=round(side * side / el, 1), unit="pairs/s", cores=1, kind="port",
-                sample=f"one {side}x{side} Kxz tile of {cfg_name} ({side*side} pairs, "
-                       f"{'f64' if dt == np.float64 else 'f32'}) through oracle/nngp_oracle.py "
-                       f"in {el:.1f} s")
+    dtn = "f64" if dt == torch.float64 else "f32"
+    res = dict(value=round(side * side / el, 1), unit="pairs/s", cores=torch.get_num_threads(),
+               kind="port", nproc=os.cpu_count(), cpu_model=cpu_info(),
+               sample=f"one {side}x{side} Kxz tile of {cfg_name} ({side * side} pairs, {dtn}) "
+                      f"through oracle/torch_cpu.py (the reference's torch op sequence) "
+                      f"in {el:.1f} s on {torch.get_num_threads()} threads")
+    cal = load_json(CALIB_FILE)
+    if cal:
+        case = next((c for c in cal["cases"] if c["config"] == cfg_name and c["dtype"] == dtn),
+                    None)
+        if case:
+            res["calibration"] = {
+                "restatement_over_reference": case["restatement_over_reference"],
+                "reference_pairs_per_s_build_container": case["reference_pairs_per_s"],
+                "threads": cal["threads"], "cpu_model": cal["cpu_model"],
+                "max_rel_diff_vs_reference": case["max_rel_diff"],
+                "source": "profiles/r2/cpu_calibration.json (tools/calibrate_cpu.py)"}
+            res["reference_equivalent_pairs_per_s"] = round(
+                res["value"] / case["restatement_over_reference"], 1)
+    return res
+
+
+def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend, probe):
+    """The step loop for one config: Kxx tiles of this rank into a device matrix."""
+    cfg = importlib.import_module(f"configs.{cfg_name}")
+    model = cfg.initial_model.to(dev, dtype)
+    C = getattr(cfg, "in_channels", 1)
+    side = 32 if C == 3 else 28
+    nb = blocks_for_world(n1, B, world)
+    n_total = nb * B if world > 1 else n1
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = torch.rand((n_total, C, side, side), generator=g, dtype=dtype).to(dev)
+    all_tiles = tile_schedule(n_total, None, B, 0, 1)
+    tiles = balanced_split(all_tiles, B, n_total, world)[rank]
+    evaluated = sum(tile_eval_pairs(t, B, n_total) for t in all_tiles)
+    ref_sched = sum(min(B, n_total - i * B) * min(B, n_total - j * B) for _, i, j in all_tiles)
+    K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
+
+    def step():
+        with torch.no_grad():
+            for same, i, j in tiles:
+                xi = X[i * B:(i + 1) * B]
+                k = model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False)
+                K[i * B:i * B + k.shape[0], j * B:j * B + k.shape[1]].copy_(k)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    from cnn_gp import netplan
+    netplan.TIMING = [] if rank == 0 and probe else None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    timing, netplan.TIMING = netplan.TIMING, None
+    return dict(model=model, X=X, K=K, n_total=n_total, tiles=tiles, all_tiles=all_tiles,
+                elapsed=elapsed, value=evaluated * steps / elapsed,
+                ref_sched_value=ref_sched * steps / elapsed, evaluated=evaluated,
+                ms_step=elapsed / steps * 1e3,
+                unique=n_total * (n_total + 1) / 2 * steps / elapsed, timing=timing)
 
 
 def main():
@@ -332,141 +398,112 @@ def main():
         else:
             dist.init_process_group(backend)
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
-
-    cfg = importlib.import_module(f"configs.{args.config}")
-    model = cfg.initial_model.to(dev, dtype)
-    C = getattr(cfg, "in_channels", 1)
-    side = 32 if C == 3 else 28
     B = args.tile
-    nb = blocks_for_world(args.n, B, world)
-    n_total = nb * B if world > 1 else args.n
-    g = torch.Generator(device="cpu").manual_seed(0)
-    X = torch.rand((n_total, C, side, side), generator=g, dtype=dtype).to(dev)
+    probe = not args.no_probe
 
-    all_tiles = tile_schedule(n_total, None, B, 0, 1)
-    tiles = balanced_split(all_tiles, B, n_total, world)[rank]
-
-    def tile_pairs(t):
-        _, i, j = t
-        return (min(B, n_total - i * B)) * (min(B, n_total - j * B))
-
-    pairs_total = sum(tile_pairs(t) for t in all_tiles)
-    K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
-
-    def step():
-        with torch.no_grad():
-            for same, i, j in tiles:
-                xi = X[i * B:(i + 1) * B]
-                if same:
-                    k = model(xi)
-                else:
-                    k = model(xi, X[j * B:(j + 1) * B], False, False)
-                K[i * B:i * B + k.shape[0], j * B:j * B + k.shape[1]].copy_(k)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    from cnn_gp import netplan
-    netplan.TIMING = [] if rank == 0 and not args.no_probe else None
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                      device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    timing, netplan.TIMING = netplan.TIMING, None
-    ms_step = elapsed / args.steps * 1e3
-    value = pairs_total * args.steps / elapsed
-
+    r = time_config(args.config, args.n, B, args.steps, args.warmup, world, rank, dev, dtype,
+                    backend, probe)
+    n_total = r["n_total"]
     extra = {}
+
     # --- solve of the assembled Kxx (single GPU) ---
     if rank == 0 and world == 1 and not args.no_solve:
+        g = torch.Generator().manual_seed(1)
         labels = torch.randint(0, 10, (n_total,), generator=g)
         Y = cnn_gp.one_hot_pm1(labels, 10).to(dev)
-        # untimed warm-up solve (rocBLAS/rocSOLVER load their kernels on first use)
-        cnn_gp.solve_system(K[:256, :256].clone(), Y[:256], jitter=1e-6)
-        Kc = K.clone()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        cnn_gp.solve_system(Kc, Y, jitter=1e-6)
-        torch.cuda.synchronize()
-        t_solve = time.perf_counter() - t1
-        extra["solve_s"] = round(t_solve, 4)
-        extra["build_solve_wall_s"] = round(ms_step / 1e3 + t_solve, 4)
-        extra["solve_gflops"] = round(n_total ** 3 / 3 / t_solve / 1e9, 1)
-        del Kc
+        # untimed warm-up solve at the full size (rocBLAS/rocSOLVER load the code objects
+        # of each blocked path on first use)
+        cnn_gp.solve_system(r["K"], Y, jitter=1e-6)
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            cnn_gp.solve_system(r["K"], Y, jitter=1e-6)      # Kxx kept: copy + factor
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t1)
+        t_solve = min(times)
+        extra["solve"] = {"n": n_total, "s": round(t_solve, 4),
+                          "tflops": round(n_total ** 3 / 3 / t_solve / 1e12, 3),
+                          "peak_tflops": FP64_PEAK_TFLOPS,
+                          "note": "dpotrf_64 + dpotrs_64 (10 rhs) on a device copy of Kxx "
+                                  "(NaN lower triangle), best of 3 after a warm-up"}
+        extra["build_solve_wall_s"] = round(r["ms_step"] / 1e3 + t_solve, 4)
 
     # --- dominant kernel, timed live ---
     roof = None
-    if rank == 0 and not args.no_probe:
-        roof = net_roofline(model, X[:B], args.config, timing)
-        # the layer-by-layer path (one HBM pass per fused op; the fallback for programs the
-        # whole-network kernel has no instantiation for): its dominant conv kernel against
-        # the HBM roof — the north star's "Conv2d covariance kernel" target
+    if rank == 0 and probe:
+        roof = net_roofline(r["model"], r["X"][:B], args.config, r["timing"])
         with torch.no_grad():
-            ops = probe_kernels(model, X[:B], B, B, reps=3)
-        by = {}
-        for name, ms, b in ops:
-            t = by.setdefault(name, [0.0, 0, 0.0, 0])
-            t[0] += ms
-            t[1] += 1
-            t[2] += b
-            t[3] = b
-        convs = {k: v for k, v in by.items() if "conv" in k} or by
-        name, (tot_ms, cnt, _, b_launch) = max(convs.items(), key=lambda kv: kv[1][0])
-        avg_ms = tot_ms / cnt
-        achieved = b_launch / (avg_ms * 1e-3) / 1e9
-        layer = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                 "kernel": name, "launches_per_tile": cnt, "avg_ms": round(avg_ms, 4),
-                 "alg_bytes_per_launch": int(b_launch),
-                 "layer_path_tile_ms": round(sum(v[0] for v in by.values()), 3),
-                 "kernel_breakdown_ms_per_tile": {k: round(v[0], 3) for k, v in by.items()}}
-        if roof is None:
-            roof = layer
-        else:
-            extra["layer_path_conv_roofline"] = layer
-        with torch.no_grad():
-            stencil = conv_stencil_roofline(model, X[:B], B)
+            stencil = conv_stencil_roofline(r["model"], r["X"][:B], B)
         if stencil is not None:
             extra["conv_stencil_roofline"] = stencil
+    del r["K"]
+    torch.cuda.empty_cache()
+
+    # --- BASELINE configs[2]: the ResNet-GP on the same harness ---
+    if not args.no_second and args.config != "mnist_as_tf":
+        r2 = time_config("mnist_as_tf", args.n, B, max(2, args.steps // 4), 1, world, rank,
+                         dev, dtype, backend, probe)
+        del r2["K"]
+        if rank == 0:
+            extra["mnist_as_tf"] = {
+                "value": round(r2["value"], 1), "unit": "pairs/s",
+                "ms_per_step": round(r2["ms_step"], 3),
+                "unique_entries_per_s": round(r2["unique"], 1),
+                "reference_schedule_pairs_per_s": round(r2["ref_sched_value"], 1),
+                "config": {"workload": f"mnist_as_tf Kxx {r2['n_total']}x{r2['n_total']}, "
+                                       f"tiles {B}", "pairs_per_step": r2["evaluated"]},
+                "roofline": net_roofline(r2["model"], r2["X"][:B], "mnist_as_tf",
+                                         r2["timing"]) if probe else None}
+        torch.cuda.empty_cache()
+
+    # --- BASELINE configs[3]: the full-scale ResNet-GP pipeline ---
+    if not args.no_fullscale and dtype == torch.float64:
+        from fullscale import fullscale
+        t0 = time.perf_counter()
+        fs = fullscale("mnist_as_tf", args.fullscale_n, args.fullscale_m, 4096, rank=rank,
+                       world=world, dev=dev)
+        if rank == 0:
+            fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
+            fs["data"] = "synthetic MNIST-like (k/255, 60% zeros, 4-px zero border)"
+            fs["note"] = ("Kxx + Kxz tiles (B=4096) split over the ranks by evaluated "
+                          "pairs, one gather per matrix to rank 0 (RCCL with nccl), "
+                          "rocSOLVER solve + predict on rank 0; spot check = single pairs "
+                          "re-evaluated through model(x_i, x_j)")
+            extra["fullscale"] = fs
+        torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.config, dtype, args.cpu_pairs)
+        cpu = cpu_baseline(args.config, dtype, args.cpu_seconds)
 
     if rank == 0:
         line = {
             "metric": "kernel entries/s (N×M pairs) + full-Kxx build+solve wall-clock, "
                       "MNIST 28×28",
-            "value": round(value, 1),
+            "value": round(r["value"], 1),
             "unit": "pairs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 3),
+            "ms_per_step": round(r["ms_step"], 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (torch.rand seed 0, 28x28x1)",
             "config": {"workload": f"{args.config} Kxx {n_total}x{n_total}, tiles {B}",
-                       "n": n_total, "tile": B, "tiles_total": len(all_tiles),
-                       "tiles_rank0": len(tiles), "pairs_per_step": pairs_total,
+                       "n": n_total, "tile": B, "tiles_total": len(r["all_tiles"]),
+                       "tiles_rank0": len(r["tiles"]), "pairs_per_step": r["evaluated"],
                        "parallelism": f"tiles-dp{world}"},
-            "unique_entries_per_s": round(n_total * (n_total + 1) / 2 * args.steps / elapsed, 1),
+            "value_counts": "pairs the device evaluates: i < j on diagonal tiles",
+            "reference_schedule_pairs_per_s": round(r["ref_sched_value"], 1),
+            "unique_entries_per_s": round(r["unique"], 1),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         line.update(extra)
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -104,6 +104,24 @@ def test_mixture_matches_reference(net):
                                        err_msg=f"{net} {dtn} {name}")
 
 
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_as_tf"])
+def test_torch_cpu_baseline_matches_reference(cfg):
+    """bench.py's CPU baseline (oracle/torch_cpu.py) computes what the reference does"""
+    import torch
+    from oracle import torch_cpu
+    z = load(f"e2e_{cfg}.npz")
+    spec = specs.CONFIGS[cfg]()
+    for pre in ("s0_uniform", "s0_mnist"):
+        X, Z = torch.from_numpy(z[pre + "_X"]), torch.from_numpy(z[pre + "_Z"])
+        for dtn, dt, tol in (("f64", torch.float64, 1e-12), ("f32", torch.float32, 2e-6)):
+            got = {"Kxx": torch_cpu.kernel(spec, X.to(dt)),
+                   "Kxz": torch_cpu.kernel(spec, X.to(dt), Z.to(dt), False, False),
+                   "Kxdiag": torch_cpu.kernel(spec, X.to(dt), X.to(dt), True, True)}
+            for name, t in got.items():
+                np.testing.assert_allclose(t.numpy(), z[f"{pre}_{dtn}_{name}"], rtol=tol,
+                                           atol=0, err_msg=f"{cfg} {pre} {dtn} {name}")
+
+
 def test_tile_schedule_matches_reference():
     z = load("tiles.npz")
     X, Z = z["X"].astype(np.float64), z["Z"].astype(np.float64)

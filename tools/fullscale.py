@@ -6,6 +6,8 @@ device, in memory.
     python tools/fullscale.py [--n 60000 --m 10000 --tile 4096 --config mnist_as_tf]
     torchrun --nproc-per-node 8 tools/fullscale.py ...   # tiles split, one gather to rank 0
 
+bench.py runs the same function as its full-scale leg (on every rank at --gpus N).
+
 Data: synthetic MNIST-like images (values k/255, ~60% zero pixels, 4-pixel zero border;
 no dataset files here) with synthetic labels, so the accuracy line only proves the path
 runs.  Kxx keeps the reference's layout (upper tiles, NaN strictly-lower tiles) and is
@@ -29,8 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import cnn_gp  # noqa: E402
-from cnn_gp.data import tile_schedule  # noqa: E402
-from cnn_gp.gram import gather_gram  # noqa: E402
+from cnn_gp.gram import gather_gram, tile_cost, tile_plan  # noqa: E402
 
 
 def mnist_like(n, C, side, seed):
@@ -49,30 +50,146 @@ def log(rank, msg):
         print(msg, flush=True)
 
 
-def build(model, X, X2, B, rank, world, out, name, t_start):
-    """This rank's tiles of Kxx (X2 None) or Kxz, written into ``out`` on the device."""
+def build(model, X, X2, B, rank, world, name, t_start, dev, out=None):
+    """This rank's tiles of Kxx (X2 None) or Kxz.  One rank: written straight into the
+    NaN-filled device matrix ``out``.  Several ranks: packed into one flat device buffer
+    (gram.gram_local's layout, split by evaluated pairs) for gather_gram.  Returns
+    (out or buffer, pairs evaluated)."""
     n = len(X)
-    tiles = tile_schedule(n, None if X2 is None else len(X2), B, rank, world)
+    n2 = None if X2 is None else len(X2)
+    split = "reference" if world == 1 else "balanced"
+    tiles = tile_plan(n, n2, B, rank, world, split)
+    if world > 1:
+        cap = max(sum(a * b for *_, a, b in tile_plan(n, n2, B, r, world, split))
+                  for r in range(world))
+        out = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
     pairs = 0
+    off = 0
     last = time.perf_counter()
     with torch.no_grad():
-        for k, (same, bi, bj) in enumerate(tiles):
-            i0, j0 = bi * B, bj * B
-            x = X[i0:i0 + B]
+        for k, (same, i0, j0, a, b) in enumerate(tiles):
+            x = X[i0:i0 + a]
             if same:
                 t = model(x)
             else:
                 src = X if X2 is None else X2
-                t = model(x, src[j0:j0 + B], False, False)
-            out[i0:i0 + t.shape[0], j0:j0 + t.shape[1]].copy_(t)
-            pairs += t.numel() if not same else t.shape[0] * (t.shape[0] + 1) // 2
+                t = model(x, src[j0:j0 + b], False, False)
+            if world > 1:
+                out[off:off + a * b].view(a, b).copy_(t)
+                off += a * b
+            else:
+                out[i0:i0 + a, j0:j0 + b].copy_(t)
+            pairs += tile_cost((same, i0, j0, a, b))
             now = time.perf_counter()
             if now - last > 20:
                 torch.cuda.synchronize()
                 log(rank, f"  {name}: tile {k + 1}/{len(tiles)} "
                           f"({time.perf_counter() - t_start:.0f} s)")
                 last = now
-    return pairs
+    return out, pairs
+
+
+def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spot=16,
+              pred_var=False, rank=0, world=1, dev=None, group=None):
+    """Kxx (n) + Kxz (m × n) + rocSOLVER solve + predict on the device; with world > 1
+    the tiles are split over the ranks and gathered once to rank 0 (one RCCL gather per
+    matrix), which solves.  Returns the result dict on rank 0, None elsewhere."""
+    dev = dev or torch.device("cuda", torch.cuda.current_device())
+    cfg = importlib.import_module(f"configs.{config}")
+    model = cfg.initial_model.to(dev, torch.float64)
+    C = getattr(cfg, "in_channels", 1)
+    side = 32 if C == 3 else 28
+    X = mnist_like(n, C, side, 0).to(dev)
+    Z = mnist_like(m, C, side, 1).to(dev)
+    g = torch.Generator().manual_seed(2)
+    ytr = torch.randint(0, 10, (n,), generator=g)
+    yte = torch.randint(0, 10, (m,), generator=g)
+    B = tile
+    res = {"config": config, "n": n, "m": m, "tile": B, "gpus": world}
+
+    if world > 1:
+        dist.barrier(group)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    K = None if world > 1 else torch.full((n, n), float("nan"), dtype=torch.float64,
+                                          device=dev)
+    K, p_xx = build(model, X, None, B, rank, world, "Kxx", t0, dev, K)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    Kxz = None if world > 1 else torch.full((m, n), float("nan"), dtype=torch.float64,
+                                            device=dev)
+    Kxz, p_xz = build(model, Z, X, B, rank, world, "Kxz", t0, dev, Kxz)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if world > 1:
+        # the slowest rank sets the build time; then ONE gather per matrix
+        dist.barrier(group)
+        t2 = time.perf_counter()
+        K = gather_gram(K, n, None, B, group)
+        Kxz = gather_gram(Kxz, m, n, B, group)
+        torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    res.update(kxx_s=round(t1 - t0, 2), kxz_s=round(t2 - t1, 2), gather_s=round(t3 - t2, 3),
+               kxx_pairs_per_s_rank0=round(p_xx / (t1 - t0), 1),
+               kxz_pairs_per_s_rank0=round(p_xz / max(t2 - t1, 1e-9), 1))
+    log(rank, f"kernels built in {t3 - t0:.1f} s")
+    if rank != 0:
+        if world > 1:
+            dist.barrier(group)
+        return None
+    # spot check: single pairs through the same drop-in call, other tile shapes
+    gs = torch.Generator().manual_seed(3)
+    ii = torch.randint(0, n, (spot,), generator=gs)
+    jj = torch.randint(0, n, (spot,), generator=gs)
+    kk = torch.randint(0, m, (spot,), generator=gs)
+    worst = 0.0
+    with torch.no_grad():
+        for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
+            a, b = min(a, b), max(a, b)
+            ref = model(X[a:a + 1], X[b:b + 1], False, False).item() if a != b else \
+                model(X[a:a + 1]).item()
+            worst = max(worst, abs(K[a, b].item() - ref) / abs(ref))
+            ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
+            worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
+    res["spot_check_max_rel_err"] = worst
+    # residual rows: K is symmetric, its upper triangle is filled
+    rows = torch.randint(0, n, (8,), generator=gs).to(dev)
+    Krows = torch.where(torch.arange(n, device=dev)[None, :] >= rows[:, None],
+                        K[rows], K[:, rows].T)
+    Y = cnn_gp.one_hot_pm1(ytr, 10).to(dev)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    A = cnn_gp.solve_system(K, Y, jitter=jitter, overwrite_a=True)   # K -> factor
+    torch.cuda.synchronize()
+    t5 = time.perf_counter()
+    diag_j = torch.arange(len(rows), device=dev)
+    Krows[diag_j, rows] += jitter
+    r = (Krows @ A - Y[rows]).norm() / Y[rows].norm()
+    pred = cnn_gp.predict(A, Kxz)
+    torch.cuda.synchronize()
+    t6 = time.perf_counter()
+    acc = cnn_gp.accuracy(pred, yte)
+    res.update(solve_s=round(t5 - t4, 2),
+               solve_tflops=round(n ** 3 / 3 / (t5 - t4) / 1e12, 2),
+               predict_s=round(t6 - t5, 3), residual=float(r),
+               synthetic_accuracy=acc, total_s=round(t6 - t0, 2))
+    if pred_var:
+        with torch.no_grad():
+            t7 = time.perf_counter()
+            kz = model(Z, Z, True, True)             # Kt_diag, save_kernel.py:33-36
+            torch.cuda.synchronize()
+            t8 = time.perf_counter()
+            var = cnn_gp.predictive_variance(K, Kxz, kz, overwrite_kxz=True)
+            torch.cuda.synchronize()
+            t9 = time.perf_counter()
+        res.update(kz_diag_s=round(t8 - t7, 3), pred_var_s=round(t9 - t8, 3),
+                   pred_var_tflops=round(n ** 2 * m / (t9 - t8) / 1e12, 2),
+                   pred_var_min=float(var.min()),
+                   pred_var_max_over_prior=float((var / kz).max()))
+    del K, Kxz
+    if world > 1:
+        dist.barrier(group)
+    return res
 
 
 def main():
@@ -94,84 +211,9 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    cfg = importlib.import_module(f"configs.{args.config}")
-    model = cfg.initial_model.to(dev, torch.float64)
-    C = getattr(cfg, "in_channels", 1)
-    side = 32 if C == 3 else 28
-    X = mnist_like(args.n, C, side, 0).to(dev)
-    Z = mnist_like(args.m, C, side, 1).to(dev)
-    g = torch.Generator().manual_seed(2)
-    ytr = torch.randint(0, 10, (args.n,), generator=g)
-    yte = torch.randint(0, 10, (args.m,), generator=g)
-    B = args.tile
-    res = {"config": args.config, "n": args.n, "m": args.m, "tile": B, "gpus": world}
-
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    K = torch.full((args.n, args.n), float("nan"), dtype=torch.float64, device=dev)
-    p_xx = build(model, X, None, B, rank, world, K, "Kxx", t0)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    Kxz = torch.full((args.m, args.n), float("nan"), dtype=torch.float64, device=dev)
-    p_xz = build(model, Z, X, B, rank, world, Kxz, "Kxz", t0)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    if world > 1:
-        K = gather_gram(K, args.n, None, B)
-        Kxz = gather_gram(Kxz, args.m, args.n, B)
-        torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    res.update(kxx_s=round(t1 - t0, 2), kxz_s=round(t2 - t1, 2), gather_s=round(t3 - t2, 3),
-               kxx_pairs_per_s_rank0=round(p_xx / (t1 - t0), 1),
-               kxz_pairs_per_s_rank0=round(p_xz / (t2 - t1), 1))
-    log(rank, f"kernels built in {t3 - t0:.1f} s")
+    res = fullscale(args.config, args.n, args.m, args.tile, args.jitter, args.spot,
+                    args.pred_var, rank, world, dev)
     if rank == 0:
-        # spot check: single pairs through the same drop-in call, other tile shapes
-        gs = torch.Generator().manual_seed(3)
-        ii = torch.randint(0, args.n, (args.spot,), generator=gs)
-        jj = torch.randint(0, args.n, (args.spot,), generator=gs)
-        kk = torch.randint(0, args.m, (args.spot,), generator=gs)
-        worst = 0.0
-        with torch.no_grad():
-            for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
-                a, b = min(a, b), max(a, b)
-                ref = model(X[a:a + 1], X[b:b + 1], a == b, False).item() if a != b else \
-                    model(X[a:a + 1]).item()
-                worst = max(worst, abs(K[a, b].item() - ref) / abs(ref))
-                ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
-                worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
-        res["spot_check_max_rel_err"] = worst
-        # residual rows: K is symmetric, its upper triangle is filled
-        rows = torch.randint(0, args.n, (8,), generator=gs).to(dev)
-        Krows = torch.where(torch.arange(args.n, device=dev)[None, :] >= rows[:, None],
-                            K[rows], K[:, rows].T)
-        Y = cnn_gp.one_hot_pm1(ytr, 10).to(dev)
-        torch.cuda.synchronize()
-        t4 = time.perf_counter()
-        A = cnn_gp.solve_system(K, Y, jitter=args.jitter, overwrite_a=True)   # K -> factor
-        torch.cuda.synchronize()
-        t5 = time.perf_counter()
-        diag_j = torch.arange(len(rows), device=dev)
-        Krows[diag_j, rows] += args.jitter
-        r = (Krows @ A - Y[rows]).norm() / Y[rows].norm()
-        pred = cnn_gp.predict(A, Kxz)
-        t6 = time.perf_counter()
-        acc = cnn_gp.accuracy(pred, yte)
-        res.update(solve_s=round(t5 - t4, 2), solve_tflops=round(args.n ** 3 / 3 / (t5 - t4) / 1e12, 2),
-                   predict_s=round(t6 - t5, 3), residual=float(r),
-                   synthetic_accuracy=acc, total_s=round(t6 - t0, 2))
-        if args.pred_var:
-            with torch.no_grad():
-                t7 = time.perf_counter()
-                kz = model(Z, Z, True, True)             # Kt_diag, save_kernel.py:33-36
-                torch.cuda.synchronize()
-                t8 = time.perf_counter()
-                var = cnn_gp.predictive_variance(K, Kxz, kz, overwrite_kxz=True)
-                torch.cuda.synchronize()
-                t9 = time.perf_counter()
-            res.update(kz_diag_s=round(t8 - t7, 3), pred_var_s=round(t9 - t8, 3),
-                       pred_var_tflops=round(args.n ** 2 * args.m / (t9 - t8) / 1e12, 2),
-                       pred_var_min=float(var.min()), pred_var_max_over_prior=float((var / kz).max()))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
