@@ -154,6 +154,24 @@ def print_timings(iterator, desc="time", print_interval=2.):
 # ------------------------------------------------------------------------------------
 # datasets (data.py:129-162) — local files only
 # ------------------------------------------------------------------------------------
+class _Transformed(torch.utils.data.Dataset):
+    """Applies a list of callables to each item's image (torchvision Compose order)."""
+
+    def __init__(self, base, transforms):
+        self.base, self.transforms = base, transforms
+
+    def __len__(self):
+        return len(self.base)
+
+    def __getitem__(self, k):
+        x, y = self.base[k]
+        for t in self.transforms:
+            x = t(x)
+        return x, y
+
+
+# ------------------------------------------------------------------------------------
+# ------------------------------------------------------------------------------------
 _MNIST_FILES = {
     True: ("train-images-idx3-ubyte", "train-labels-idx1-ubyte"),
     False: ("t10k-images-idx3-ubyte", "t10k-labels-idx1-ubyte"),
@@ -199,18 +217,91 @@ def load_mnist(root: str, train: bool):
         "(this build never downloads; place the files there)")
 
 
+_CIFAR_BIN = ("cifar-10-batches-bin",
+              tuple(f"data_batch_{k}.bin" for k in range(1, 6)), ("test_batch.bin",))
+_CIFAR_PY = ("cifar-10-batches-py",
+             tuple(f"data_batch_{k}" for k in range(1, 6)), ("test_batch",))
+
+
+def _cifar_bin(path):
+    """One CIFAR-10 binary batch: records of 1 label byte + 3072 pixel bytes (the R, G
+    and B 32x32 planes, row-major)."""
+    raw = np.fromfile(path, dtype=np.uint8)
+    if raw.size % 3073:
+        raise ValueError(f"{path}: not a CIFAR-10 binary batch ({raw.size} bytes)")
+    rec = raw.reshape(-1, 3073)
+    return rec[:, 1:].reshape(-1, 3, 32, 32), rec[:, 0].astype(np.int64)
+
+
+class _ArrayOnlyUnpickler:
+    """Unpickler for the CIFAR-10 python batches that resolves only numpy's array
+    reconstruction (the batches hold a dict of bytes keys, a uint8 array and a label
+    list); any other global in the file is refused."""
+    _ALLOWED = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray",
+                                                              "_reconstruct"),
+                ("numpy", "ndarray"), ("numpy", "dtype")}
+
+    @classmethod
+    def load(cls, f):
+        import pickle
+
+        class U(pickle.Unpickler):
+            def find_class(self, module, name):
+                if (module, name) not in cls._ALLOWED:
+                    raise pickle.UnpicklingError(f"refusing {module}.{name}")
+                return super().find_class(module, name)
+        return U(f, encoding="bytes").load()
+
+
+def _cifar_py(path):
+    with open(path, "rb") as f:
+        d = _ArrayOnlyUnpickler.load(f)
+    x = np.asarray(d[b"data"], dtype=np.uint8).reshape(-1, 3, 32, 32)
+    return x, np.asarray(d[b"labels"], dtype=np.int64)
+
+
+def load_cifar10(root: str, train: bool):
+    """CIFAR-10 as torchvision's CIFAR10 + ToTensor() sees it: float32 in [0, 1],
+    [N, 3, 32, 32] (channel planes R, G, B), int64 labels; train = the 5 data batches in
+    order (50 000), test = test_batch (10 000).  Reads the binary distribution
+    (cifar-10-batches-bin) or the python one torchvision downloads (cifar-10-batches-py)
+    under root/; never downloads."""
+    for sub, trn, tst, reader in (_CIFAR_BIN + (_cifar_bin,), _CIFAR_PY + (_cifar_py,)):
+        files = [os.path.join(root, sub, f) for f in (trn if train else tst)]
+        if all(os.path.exists(f) for f in files):
+            parts = [reader(f) for f in files]
+            x = np.concatenate([p[0] for p in parts])
+            y = np.concatenate([p[1] for p in parts])
+            return TensorDataset(torch.from_numpy(x.astype(np.float32) / 255.0),
+                                 torch.from_numpy(y))
+    raise FileNotFoundError(
+        f"CIFAR-10 batches not found under {root} (cifar-10-batches-bin/ or "
+        "cifar-10-batches-py/; this build never downloads)")
+
+
+_LOADERS = {"MNIST": load_mnist, "CIFAR10": load_cifar10}
+
+
 class DatasetFromConfig:
     """train/validation/test Subsets of ConcatDataset([train, test]) by the config's
-    ranges (data.py:134-158).  Reads local files; supports dataset_name "MNIST"."""
+    ranges (data.py:134-158).  Reads local files of config.dataset_name: "MNIST" (IDX)
+    or "CIFAR10" (binary or python batches), from datasets_path/<dataset_name>/ like
+    the reference.  Extra config.transforms are applied per item like torchvision's
+    Compose after ToTensor."""
 
     def __init__(self, datasets_path, config):
         self.config = config
         name = getattr(config, "dataset_name", "MNIST")
         root = os.path.join(datasets_path, name)
-        if name != "MNIST":
-            raise NotImplementedError(f"dataset {name!r}: only local MNIST IDX is supported")
-        train_full = load_mnist(root, True)
-        test_full = load_mnist(root, False)
+        if name not in _LOADERS:
+            raise NotImplementedError(f"dataset {name!r}: local MNIST and CIFAR10 are "
+                                      "supported")
+        train_full = _LOADERS[name](root, True)
+        test_full = _LOADERS[name](root, False)
+        transforms = list(getattr(config, "transforms", []) or [])
+        if transforms:
+            train_full, test_full = (_Transformed(d, transforms)
+                                     for d in (train_full, test_full))
         self.data_full = ConcatDataset([train_full, test_full])
         self.train = Subset(self.data_full, config.train_range)
         self.validation = Subset(self.data_full, config.validation_range)
@@ -218,4 +309,5 @@ class DatasetFromConfig:
 
     @staticmethod
     def load_full(dataset):
+        """(images, labels) of a whole dataset in one batch (data.py:160-162)."""
         return next(iter(DataLoader(dataset, batch_size=len(dataset))))

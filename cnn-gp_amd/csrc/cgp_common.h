@@ -212,6 +212,10 @@ __device__ __forceinline__ T relu_fast(T c, T v1, T v2, const PolyTab& tab) {
 // Horner steps are inline asm, which the scheduler keeps in source order, so a per-pixel
 // loop would run R dependent 16-step chains back to back; interleaved here, every step
 // has R independent FMAs in flight.  Same arithmetic as relu_fast(c, v1, v2, tab).
+// |rho| clamped to 1 - 2^-52 (not 1) keeps x = (1 - |rho|)/2 >= 2^-53, so rsq(x) is
+// finite without a floor on x: one op less per pixel; where |rho| >= 1 - 2^-52 the x^1.5
+// term is below 1e-23 of sqrt(t)
+constexpr double kRhoMax = 1.0 - 0x1p-52;
 template <int R>
 __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R],
                                             const double (&v2)[R], const PolyTab& tab) {
@@ -224,9 +228,9 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        a[r] = __builtin_fmin(__builtin_fabs(c[r] * y[r]), 1.0);
+        a[r] = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);
         u[r] = __builtin_fma(-0.5, a[r], 0.5);
-        sx[r] = (st[r] * u[r]) * sqrt_fast(__builtin_fmax(u[r], K<double>::xfloor));
+        sx[r] = (st[r] * u[r]) * sqrt_fast(u[r]);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) p[r] = fma_sc(tab.d[kReluPolyDegD], u[r], tab.d[kReluPolyDegD - 1]);

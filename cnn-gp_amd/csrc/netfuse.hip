@@ -183,6 +183,47 @@ __device__ __forceinline__ int opaque_tid() {
     return t;
 }
 
+// a / d for a >= 0 as an unsigned division (a constant d costs a mul-hi and a shift; the
+// signed form needs three more fix-up ops)
+__device__ __forceinline__ int udiv(int a, int d) { return (int)((unsigned)a / (unsigned)d); }
+
+// the op table through the constant address space: the kernel never writes it, so its
+// fields load with scalar loads into SGPRs (a generic pointer gets per-lane vector loads
+// because stores to the output could alias it)
+#ifndef CGP_NET_SCALAR_OPS
+#define CGP_NET_SCALAR_OPS 0
+#endif
+#if CGP_NET_SCALAR_OPS
+typedef const __attribute__((address_space(4))) cgp_net_op* OpsC;
+#else
+typedef const cgp_net_op* OpsC;
+#endif
+__device__ __forceinline__ OpsC ops_c(const cgp_net_op* p) { return (OpsC)p; }
+__device__ __forceinline__ cgp_net_op load_op(OpsC r) {
+    cgp_net_op o;
+    o.kind = r->kind;
+    o.code = r->code;
+    o.src = r->src;
+    o.dst = r->dst;
+    o.add = r->add;
+    o.ws_in = r->ws_in;
+    o.ws_out = r->ws_out;
+    o.relu = r->relu;
+    o.h = r->h;
+    o.w = r->w;
+    o.div_m = r->div_m;
+    o.div_s = r->div_s;
+    o.dst2 = r->dst2;
+    o.zero_halo = r->zero_halo;
+    o.weight = r->weight;
+    o.bias = r->bias;
+    o.var_x = r->var_x;
+    o.var_y = r->var_y;
+    o.var2_x = r->var2_x;
+    o.var2_y = r->var2_y;
+    return o;
+}
+
 // global-address-space views: pointers read from the op table are generic, and flat
 // loads would also count in lgkmcnt, so every LDS wait would drain them
 template <typename T>
@@ -344,7 +385,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int k = 0; k < (G::HW + kNT - 1) / kNT; ++k) {
             const int px = tid + k * kNT;
             if (G::HW % kNT == 0 || px < G::HW) {
-                const int r = px / G::W, c = px - r * G::W;
+                const int r = udiv(px, G::W), c = px - r * G::W;
                 acc += src[r * wsi + c];
             }
         }
@@ -371,14 +412,14 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // segmented butterfly; the group's first lane finishes the pair
         constexpr int TPP = kNT / NP;
         static_assert(TPP <= 64 && kNT % NP == 0, "reduce groups must not straddle waves");
-        const int q = tid / TPP, lane = tid - q * TPP;
+        const int q = udiv(tid, TPP), lane = tid - q * TPP;
         const T* srcq = src + q * arena;
         T acc = T(0);
 #pragma unroll
         for (int k = 0; k < (G::HW + TPP - 1) / TPP; ++k) {
             const int px = lane + k * TPP;
             if (G::HW % TPP == 0 || px < G::HW) {
-                const int r = px / G::W, c = px - r * G::W;
+                const int r = udiv(px, G::W), c = px - r * G::W;
                 acc += srcq[r * wsi + c];
             }
         }
@@ -407,12 +448,12 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             const int e = tid + k * kNT;
             ok[k] = N % kNT == 0 || e < N;
             const int ec = ok[k] ? e : 0;
-            const int q = NP == 1 ? 0 : ec / G::HOWO, pc = ec - q * G::HOWO;
-            const int r = pc / G::WO, c = pc - r * G::WO;
+            const int q = NP == 1 ? 0 : udiv(ec, G::HOWO), pc = ec - q * G::HOWO;
+            const int r = udiv(pc, G::WO), c = pc - r * G::WO;
             const VarSrc<T> vs = vs_of(q);
             at[k] = q * arena + r * wso + c;
-            u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
-            u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
+            u1[k] = (vs.on && ok[k]) ? vs.x[(unsigned)pc] : T(1);
+            u2[k] = (vs.on && ok[k]) ? vs.y[(unsigned)pc] : T(1);
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
         net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
@@ -427,13 +468,13 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
             const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
-            const int q = NP == 1 ? 0 : itc / G::NV, l = itc - q * G::NV;
-            const int g3 = l / G::WO, c = l - g3 * G::WO;
+            const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
+            const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
             const VarSrc<T> vs = vs_of(q);
 #pragma unroll
             for (int k = 0; k < G::R3; ++k) {
-                u1[kv][k] = vs.on ? vs.x[(g3 * G::R3 + k) * G::WO + c] : T(1);
-                u2[kv][k] = vs.on ? vs.y[(g3 * G::R3 + k) * G::WO + c] : T(1);
+                u1[kv][k] = vs.on ? vs.x[(unsigned)((g3 * G::R3 + k) * G::WO + c)] : T(1);
+                u2[kv][k] = vs.on ? vs.y[(unsigned)((g3 * G::R3 + k) * G::WO + c)] : T(1);
             }
         }
         // outputs that land on the source (in place, or dst2 on the source) are stored
@@ -448,8 +489,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
             if (NVT % kNT == 0 || it < NVT) {
-                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
-                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
+                const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const T* base = src + q * arena + c * G::S + G::OFF;
                 const int r0 = g3 * G::R3 * G::S + G::OFF;
                 T rs[G::WIN3];
@@ -478,8 +519,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
             if (NVT % kNT == 0 || it < NVT) {
-                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
-                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
+                const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 int at[G::R3];
                 bool ok[G::R3];
 #pragma unroll
@@ -500,13 +541,13 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             for (int kv = 0; kv < G::KV; ++kv) {
                 const int it = tid + kv * kNT;
                 const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
-                const int q = NP == 1 ? 0 : itc / G::NV, l = itc - q * G::NV;
-                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
+                const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const VarSrc<T> vs = vs_of(q);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
-                    u1[kv][k] = vs.x[(g3 * G::R3 + k) * G::WO + c];
-                    u2[kv][k] = vs.y[(g3 * G::R3 + k) * G::WO + c];
+                    u1[kv][k] = vs.x[(unsigned)((g3 * G::R3 + k) * G::WO + c)];
+                    u2[kv][k] = vs.y[(unsigned)((g3 * G::R3 + k) * G::WO + c)];
                 }
             }
         } else {
@@ -520,8 +561,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int kh = 0; kh < G::KH; ++kh) {
             const int it = tid + kh * kNT;
             if (NHT % kNT == 0 || it < NHT) {
-                const int q = NP == 1 ? 0 : it / G::NH, l = it - q * G::NH;
-                const int qi = l / G::NG2, g2 = l - qi * G::NG2;
+                const int q = NP == 1 ? 0 : udiv(it, G::NH), l = it - q * G::NH;
+                const int qi = udiv(l, G::NG2), g2 = l - qi * G::NG2;
                 const T* row = src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
                                g2 * G::R2 * G::S + G::OFF;
                 T win[G::WIN2];
@@ -540,7 +581,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             for (int z0 = 0; z0 < NZT; z0 += kNT) {
                 const int z = z0 + tid;
                 if (NZT % kNT == 0 || z < NZT) {
-                    const int q = NP == 1 ? 0 : z / G::NZ, zl = z - q * G::NZ;
+                    const int q = NP == 1 ? 0 : udiv(z, G::NZ), zl = z - q * G::NZ;
                     hs[q * arena + (zl < G::Q0 * G::WO ? zl : zl + G::NVR * G::WO)] = T(0);
                 }
             }
@@ -552,8 +593,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * kNT;
             if (NVT % kNT == 0 || it < NVT) {
-                const int q = NP == 1 ? 0 : it / G::NV, l = it - q * G::NV;
-                const int g3 = l / G::WO, c = l - g3 * G::WO;
+                const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
+                const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const T* col = hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
                 T win[G::WIN3];
 #pragma unroll
@@ -612,7 +653,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         ok[k] = e < n;
         const int ec = ok[k] ? e : 0;
         const int q = NP == 1 ? 0 : ec / hw, pc = ec - q * hw;
-        const int r = W_ ? pc / W_ : (int)fdiv((unsigned)pc, fw);
+        const int r = W_ ? udiv(pc, W_) : (int)fdiv((unsigned)pc, fw);
         at[k] = q * arena + r * ws + (pc - r * wd);
         VarSrc<T> vs = vs0;
         if constexpr (NP > 1) {
@@ -620,15 +661,15 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             pair_q<NP>(pr, q, iq, jq);
             vs = vs_of(iq, jq);
         }
-        u1[k] = (vs.on && ok[k]) ? vs.x[pc] : T(1);
-        u2[k] = (vs.on && ok[k]) ? vs.y[pc] : T(1);
+        u1[k] = (vs.on && ok[k]) ? vs.x[(unsigned)pc] : T(1);
+        u2[k] = (vs.on && ok[k]) ? vs.y[(unsigned)pc] : T(1);
         if constexpr (KIND == CGP_NET_RELU) {
             a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
             T acc = xi[pc] * yj[pc];
             for (int ch = 1; ch < p.channels; ++ch)
                 acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
-            a[k] = acc / T(p.channels);
+            a[k] = p.channels == 1 ? acc : acc / T(p.channels);   // x / 1 == x
         } else {
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
         }
@@ -860,7 +901,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
     constexpr ProgInfo I = kProgs[PID];
     if constexpr (K < I.nops) {
         constexpr ProgOp o = kProgOps[I.first + K];
-        const cgp_net_op& rt = p.ops[K];
+        const auto& rt = ops_c(p.ops)[K];
         cgp_net_op op;
         op.kind = o.kind;
         op.code = o.code;
@@ -1003,7 +1044,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         if constexpr (PID < 0) {
             for (int k = 0; k < p.nops; ++k) {
-                const cgp_net_op op = p.ops[k];
+                const cgp_net_op op = load_op(ops_c(p.ops) + k);
                 net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
                 lds_barrier();
             }

@@ -73,7 +73,7 @@ def _samples(rng, chunk, st, same_tile_n, n1, n2, same, count):
     return out
 
 
-@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_as_tf"])
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_as_tf", "cifar10"])
 @pytest.mark.parametrize("numerics", ["fast", "exact"])
 def test_bench_geometry_sampled_entries_vs_oracle(cfg, numerics, monkeypatch):
     from cnn_gp import gram, netplan

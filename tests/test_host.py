@@ -252,6 +252,70 @@ def test_idx_reader(tmp_path):
     np.testing.assert_array_equal(read_idx(str(tmp_path / "t.idx")), imgs)
 
 
+def _cifar_fixture(root, fmt, rng):
+    """5 train batches of 3 images + a test batch of 2, in the binary or python format"""
+    import pickle
+    batches = {}
+    names = [f"data_batch_{k}" for k in range(1, 6)] + ["test_batch"]
+    for k, name in enumerate(names):
+        n = 2 if name == "test_batch" else 3
+        x = rng.integers(0, 256, size=(n, 3072), dtype=np.uint8)
+        y = rng.integers(0, 10, size=n).astype(np.uint8)
+        batches[name] = (x, y)
+        if fmt == "bin":
+            d = root / "CIFAR10" / "cifar-10-batches-bin"
+            d.mkdir(parents=True, exist_ok=True)
+            (d / (name + ".bin")).write_bytes(np.concatenate([y[:, None], x], 1).tobytes())
+        else:
+            d = root / "CIFAR10" / "cifar-10-batches-py"
+            d.mkdir(parents=True, exist_ok=True)
+            with open(d / name, "wb") as f:
+                pickle.dump({b"batch_label": name.encode(), b"labels": [int(v) for v in y],
+                             b"data": x, b"filenames": [b"f"] * n}, f)
+    return batches, names
+
+
+@pytest.mark.parametrize("fmt", ["bin", "py"])
+def test_cifar10_dataset_from_config(tmp_path, fmt):
+    """DatasetFromConfig for CIFAR10 (data.py:143-158): ConcatDataset(train 5 batches,
+    test batch), ToTensor's float32/255 in [3,32,32] R,G,B planes, Subsets by the
+    config's ranges (configs/cifar10.py:4-6 pattern, scaled to the fixture)"""
+    import types
+    from cnn_gp.data import DatasetFromConfig
+    rng = np.random.default_rng(3)
+    batches, names = _cifar_fixture(tmp_path, fmt, rng)
+    cfg = types.SimpleNamespace(dataset_name="CIFAR10", train_range=range(12),
+                                validation_range=range(12, 15), test_range=range(15, 17),
+                                transforms=[])
+    ds = DatasetFromConfig(str(tmp_path), cfg)
+    assert len(ds.data_full) == 17 and len(ds.train) == 12 and len(ds.test) == 2
+    allx = np.concatenate([batches[n][0] for n in names]).reshape(-1, 3, 32, 32)
+    ally = np.concatenate([batches[n][1] for n in names])
+    X, Y = DatasetFromConfig.load_full(ds.test)
+    assert X.dtype == torch.float32 and X.shape == (2, 3, 32, 32)
+    np.testing.assert_array_equal(X.numpy(), allx[15:17].astype(np.float32) / 255)
+    np.testing.assert_array_equal(Y.numpy(), ally[15:17])
+    Xv, _ = DatasetFromConfig.load_full(ds.validation)
+    np.testing.assert_array_equal(Xv.numpy(), allx[12:15].astype(np.float32) / 255)
+    # config transforms run after ToTensor, per item
+    cfg.transforms = [lambda t: t * 2]
+    X2, _ = DatasetFromConfig.load_full(DatasetFromConfig(str(tmp_path), cfg).test)
+    np.testing.assert_array_equal(X2.numpy(), 2 * X.numpy())
+
+
+def test_cifar10_python_batches_refuse_foreign_globals(tmp_path):
+    import pickle
+    from cnn_gp.data import load_cifar10
+    d = tmp_path / "cifar-10-batches-py"
+    d.mkdir()
+    for name in [f"data_batch_{k}" for k in range(1, 6)]:
+        with open(d / name, "wb") as f:
+            pickle.dump({b"data": np.zeros((1, 3072), np.uint8), b"labels": [0],
+                         b"evil": os.system}, f)
+    with pytest.raises(pickle.UnpicklingError):
+        load_cifar10(str(tmp_path), True)
+
+
 def test_print_timings_passthrough(capsys):
     from cnn_gp.data import print_timings
     assert list(print_timings([1, 2, 3], print_interval=0.0)) == [1, 2, 3]
