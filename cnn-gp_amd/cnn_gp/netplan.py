@@ -45,6 +45,9 @@ TIMING = None
 # the reference configs' lowered programs, every offset an immediate).  False forces the
 # op-record interpreter (A/B and parity tests of both paths).
 USE_PROGRAMS = os.environ.get("CGP_NET_PROGRAMS", "1") != "0"
+# quartered x-side variance maps for the fp64 closed-form ReLU (relu_q_n); 0 only to time
+# library builds that predate it (tools/variants.sh)
+QUARTER_MAPS = os.environ.get("CGP_NET_QUARTER", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
 
 
@@ -538,6 +541,22 @@ class NetPlan:
         fn = getattr(lib, f"cgp_net_{sfx}")
         launches = []
         keep = []
+        # the fp64 closed-form ReLU (csrc/cgp_common.h relu_q_n) reads the x-side variance
+        # maps quartered (an exact scaling that folds its Newton steps' halvings); the
+        # copies are filled on the launch stream before the kernels
+        quarters = []
+        if x.dtype == torch.float64 and not flags & N.CGP_FLAG_EXACT_RELU and QUARTER_MAPS:
+            used = set()
+            for st in self.stages:
+                used |= {v for _, v in st.records if v is not None}
+                used |= {f["var2"] for f, _ in st.records if "var2" in f}
+            var = dict(var)
+            for v in sorted(used):
+                vx, vy = var[v]
+                q = torch.empty_like(vx)
+                quarters.append((vx, q))
+                keep.append(q)
+                var[v] = (q, vy)
         for sidx, st in enumerate(self.stages):
             arr = self._ops_array(st, var, states[sidx], states[sidx + 1])
             host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
@@ -562,6 +581,9 @@ class NetPlan:
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2
 
         def run_all(stream):
+            for src, q in quarters:
+                N.call("cgp_axpby_f64", 0.25, N.ptr(src), 0.0, None, N.ptr(q), src.numel(),
+                       stream)
             for u0 in range(0, units, chunk):
                 u1 = min(units, u0 + chunk)
                 for a in launches:

@@ -167,15 +167,26 @@ static __constant__ double kReluPolyTabD[kReluPolyDegD + 1] = {
     CGP_C(8), CGP_C(9), CGP_C(10), CGP_C(11), CGP_C(12), CGP_C(13)};
 #undef CGP_C
 static_assert(kReluPolyDegD == 13, "kReluPolyTabD lists 14 coefficients");
+// P̃(x4) = P(x4/4)/16: coefficient k scaled by 1/(16·4^k), exact powers of two, so Horner in
+// x4 = 4x rounds exactly like Horner in x (relu_q_n)
+constexpr double poly_q(int k) {
+    double v = kReluPolyD[k] * 0.0625;
+    for (int n = 0; n < k; ++n) v *= 0.25;
+    return v;
+}
+static __constant__ double kReluPolyTabDq[kReluPolyDegD + 1] = {
+    poly_q(0), poly_q(1), poly_q(2), poly_q(3), poly_q(4), poly_q(5), poly_q(6),
+    poly_q(7), poly_q(8), poly_q(9), poly_q(10), poly_q(11), poly_q(12), poly_q(13)};
 
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
-    ConstD d;
+    ConstD d, dq;
 };
 __device__ __forceinline__ PolyTab poly_table() {
     ConstD p = (ConstD)kReluPolyTabD;
-    asm volatile("" : "+s"(p));
-    return PolyTab{p};
+    ConstD q = (ConstD)kReluPolyTabDq;
+    asm volatile("" : "+s"(p), "+s"(q));
+    return PolyTab{p, q};
 }
 // r·u + c with c in an SGPR pair: the VOP3 form (the compiler would copy c to VGPRs
 // for v_fmac_f64 instead)
@@ -243,6 +254,52 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 #pragma unroll
     for (int r = 0; r < R; ++r)
         c[r] = __builtin_fma(sx[r], p[r], (c[r] + __builtin_fabs(c[r])) * 0.25);
+}
+// The map of relu_fast_n in the form the whole-network kernel runs (28 VALU ops + 2 rsq
+// per pixel instead of 31): every 1/2 of the two Newton steps and the output's 1/4 is
+// folded into a power-of-two scaling of an input or a coefficient, so each Newton step
+// costs 4 ops.  A refinement y = y0(1 + e/2), e = 1 - A·y0², of y0 ≈ rsq(A) is
+// y = r·(3 − m·r) with r = rsq(4A) ≈ y0/2 and m = 4A·r — and 4A·r·(3 − m·r) = 4·sqrt(A).
+// Inputs, all exact scalings of relu_fast's:
+//   v1q = v1/4 (the x-side variance map, quartered by the host; netplan.py),
+//   cq  = c/4  (QIN: the producing conv already applied w/4 and b/4; else one multiply),
+// then T = v1q·v2 + tiny/4 = t/4 gives r = rsq(T) ≈ 2/sqrt(t): Y = r·(3 − T·r·r) = 4/sqrt(t),
+// sqrt(t) = T·r·(3 − T·r·r), and |cq|·Y = |c|/sqrt(t) = |rho|.  With x4 = 4x = 2 − 2|rho|,
+// 4·sqrt(x) = x4·h·(3 − x4·h·h), h = rsq(x4), the polynomial term is
+// sqrt(t)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/16 at x4/4, and max(c, 0)/2 = cq + |cq|.
+template <int R, bool QIN>
+__device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
+                                         const double (&v2)[R], const PolyTab& tab) {
+    double y[R], st[R], sx[R], u[R], p[R];   // u: x4
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if constexpr (!QIN) c[r] *= 0.25;
+        const double T = __builtin_fma(v1q[r], v2[r], 0.25 * K<double>::tiny);
+        const double r0 = __builtin_amdgcn_rsq(T);
+        const double m = T * r0;
+        const double k = __builtin_fma(-m, r0, 3.0);
+        y[r] = r0 * k;
+        st[r] = m * k;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double a = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);
+        u[r] = __builtin_fma(-2.0, a, 2.0);
+        const double h = __builtin_amdgcn_rsq(u[r]);
+        const double m = u[r] * h;
+        const double sq4 = m * __builtin_fma(-m, h, 3.0);
+        sx[r] = (st[r] * u[r]) * sq4;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) p[r] = fma_sc(tab.dq[kReluPolyDegD], u[r], tab.dq[kReluPolyDegD - 1]);
+#pragma unroll
+    for (int k = kReluPolyDegD - 2; k >= 0; --k) {
+        const double ck = tab.dq[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = __builtin_fma(sx[r], p[r], c[r] + __builtin_fabs(c[r]));
 }
 template <int R>
 __device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],

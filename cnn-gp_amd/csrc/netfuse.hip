@@ -281,13 +281,21 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
     else
         return relu_fast(c, v1, v2, tab);
 }
-// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k])
-template <bool EXACT, typename T, int R>
+// The fp64 closed form reads quartered x-side variance maps (relu_q_n; the host passes
+// v/4 maps for f64 launches without CGP_FLAG_EXACT_RELU) and, when the producing conv
+// scaled its weight and bias by 1/4 (QIN), a quartered input.
+template <typename T, bool EX>
+constexpr bool kQuarter = !EX && sizeof(T) == 8;
+
+// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4)
+template <bool EXACT, bool QIN, typename T, int R>
 __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
                                        const PolyTab& tab) {
     if constexpr (EXACT) {
 #pragma unroll
         for (int k = 0; k < R; ++k) v[k] = relu_exact_inl(v[k], u1[k], u2[k]);
+    } else if constexpr (sizeof(T) == 8) {
+        relu_q_n<R, QIN>(v, u1, u2, tab);
     } else {
         relu_fast_n<R>(v, u1, u2, tab);
     }
@@ -320,7 +328,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
                                         const int (&at)[R], const bool (&ok)[R],
                                         const T (&u1)[R], const T (&u2)[R],
                                         const PolyTab& tab) {
-    if (op.relu) relu_n<EX, T, R>(v, u1, u2, tab);
+    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, R>(v, u1, u2, tab);
     if (op.add >= 0) {
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -330,7 +338,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
     for (int k = 0; k < R; ++k)
         if (ok[k]) lds[op.dst + at[k]] = v[k];
     if (DU && op.dst2 >= 0) {
-        relu_n<EX, T, R>(v, u1, u2, tab);
+        relu_n<EX, false, T, R>(v, u1, u2, tab);
 #pragma unroll
         for (int k = 0; k < R; ++k)
             if (ok[k]) lds[op.dst2 + at[k]] = v[k];
@@ -363,7 +371,9 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     constexpr int NP = G::NP;
     const int tid = opaque_tid();
     const PolyTab tab = poly_table();
-    const T w = T(op.weight), b = T(op.bias);
+    // a conv feeding the fp64 closed-form ReLU produces c/4 (exact: w/4, b/4) for relu_q_n
+    const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
+    const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
     const VarSrc<T> vs0 = var_src<T>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
@@ -675,7 +685,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         }
     }
     if constexpr (KIND == CGP_NET_RELU) {
-        if (live) relu_n<EX, T, KE>(a, u1, u2, tab);
+        if (live) relu_n<EX, false, T, KE>(a, u1, u2, tab);
         if (op.add >= 0) {
 #pragma unroll
             for (int k = 0; k < KE; ++k)
@@ -687,7 +697,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         if (ok[k]) lds[op.dst + at[k]] = a[k];
     if constexpr (KIND == CGP_NET_LINEAR && DU) {
         if (op.dst2 >= 0) {
-            if (live) relu_n<EX, T, KE>(a, u1, u2, tab);
+            if (live) relu_n<EX, false, T, KE>(a, u1, u2, tab);
 #pragma unroll
             for (int k = 0; k < KE; ++k)
                 if (ok[k]) lds[op.dst2 + at[k]] = a[k];

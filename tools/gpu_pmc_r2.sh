@@ -20,7 +20,7 @@ run() {   # tag counters cmd...
 for cfg in $CFGS; do
     run ${cfg}_fetch "FETCH_SIZE" python3 tools/netbench.py --configs $cfg --reps 1
     run ${cfg}_write "WRITE_SIZE" python3 tools/netbench.py --configs $cfg --reps 1
-    run ${cfg}_sq "$SQ" python3 tools/netbench.py --configs $cfg --reps 1
+    run ${cfg}_sq "$SQ GRBM_GUI_ACTIVE" python3 tools/netbench.py --configs $cfg --reps 1
 done
 run stencil_fetch "FETCH_SIZE" python3 tools/stencil_once.py
 run stencil_write "WRITE_SIZE" python3 tools/stencil_once.py

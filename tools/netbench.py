@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--configs", default="mnist_paper_convnet_gp,mnist_paper_residual_cnn_gp,"
                                          "mnist_as_tf,cifar10")
     ap.add_argument("--same", action="store_true", help="Kxx diagonal tile (i<j pairs)")
+    ap.add_argument("--data", default="rand", choices=["rand", "zeros", "half"],
+                    help="image data: uniform, all zero, or every pixel 0.5 (switching-"
+                         "activity probe: the arithmetic is the same, the toggling is not)")
     ap.add_argument("--per-stage", action="store_true",
                     help="also time each stage's launches (multi-pair stages)")
     args = ap.parse_args()
@@ -38,6 +41,10 @@ def main():
         g = torch.Generator().manual_seed(0)
         X = torch.rand((B, C, side, side), generator=g, dtype=dt).cuda()
         Z = X if args.same else torch.rand((B, C, side, side), generator=g, dtype=dt).cuda()
+        if args.data != "rand":
+            v = 0.0 if args.data == "zeros" else 0.5
+            X = torch.full_like(X, v)
+            Z = X if args.same else torch.full_like(Z, v)
         plan = m._plan(side, side)
         net = m._net_plan(plan, X.element_size())
         assert net is not None, name

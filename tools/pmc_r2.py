@@ -79,6 +79,10 @@ def main():
             "kernel_ms_per_tile_under_pmc": ms / evals,
             "valu_issue_frac_under_pmc": 4 * sq["SQ_ACTIVE_INST_VALU"] /
                                          (1024 * 2.4e9 * ms * 1e-3),
+            # GRBM_GUI_ACTIVE: GPU-busy cycles of the dispatches (summed over the XCDs'
+            # records); cycles / duration = the engine clock the kernel actually ran at
+            "grbm_gui_active": sq.get("GRBM_GUI_ACTIVE"),
+            "grbm_records": nsq.get("GRBM_GUI_ACTIVE"),
             "source": f"rocprofv3 --pmc, tools/gpu_pmc_r2.sh on {cfg} (B={TILE} Kxz tile x "
                       f"{evals}); bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
         }
