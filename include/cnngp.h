@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 5
+#define CGP_ABI_VERSION 6
 
 /* error codes */
 #define CGP_OK 0
@@ -256,7 +256,9 @@ typedef struct cgp_net_op {
                               another slot used as data (the LDS arena is shared across
                               map sizes). */
     double weight, bias;   /* CONV: w·Σ + b;  LINEAR: dst = weight·src + bias·add */
-    const void* var_x;     /* ReLU input variances of the x images, [n1][h·w] */
+    const void* var_x;     /* ReLU input variances of the x images, [n1][h·w]; for
+                              cgp_net_f64 without CGP_FLAG_EXACT_RELU: QUARTERED (v/4, the
+                              scaled closed form; var2_x likewise) */
     const void* var_y;     /* ... of the y images, [n2][h·w] */
     const void* var2_x;    /* dst2's ReLU: variances of the result, [n1][h·w] */
     const void* var2_y;    /* [n2][h·w] */
@@ -310,6 +312,7 @@ int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pai
  * (net_programs.h); a program kernel runs them with every offset an immediate. */
 int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t flags,
                     int32_t lds_elems, int32_t itemsize);
+/* ABI 6: cgp_net_f64's fast path reads var_x / var2_x quartered (see cgp_net_op). */
 int cgp_net_f64(const cgp_net_args* args, void* stream);
 int cgp_net_f32(const cgp_net_args* args, void* stream);
 
