@@ -191,7 +191,7 @@ def gather_gram(local: torch.Tensor, N: int, N2: Optional[int], batch_size: int,
     if staged:
         send = send.cpu()
     gathered = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
-    dist.gather(send, gathered, dst=dst, group=group)
+    dist.gather(send, gathered, group=group, group_dst=dst)   # dst: a rank of `group`
     if rank != dst:
         return None
     full = torch.full((N, n2), float("nan"), dtype=local.dtype, device=local.device)
