@@ -104,6 +104,18 @@ class Stage:
 
 # pairs per workgroup of a stage whose maps are all at most this many pixels
 MULTI_PAIR = ((16, 64), (4, 256))
+# pairs per workgroup of the first stage (the full-size maps): 2 runs two one-pair halves
+# in one four-wave workgroup (csrc/netfuse.hip net_kernel, NP == 2: units u and u + 1, the
+# same image i), 1 one pair on two waves.  Measured on the MI355X (one B = 1024 Kxz tile):
+# ConvNet GP +13%, mnist_as_tf / cifar10 +1%, Residual CNN GP even.  CGP_NET_PAIRS0=1
+# selects one pair per workgroup.
+FIRST_PAIRS = os.environ.get("CGP_NET_PAIRS0", "2")
+
+
+def first_pairs(n_stages: int) -> int:
+    """Pairs per workgroup of the first of n_stages stages."""
+    del n_stages
+    return 2 if FIRST_PAIRS in ("2", "auto") else 1
 MIN_STAGE_OPS = 4                      # a shorter tail is not worth a launch + state
 CHUNK_BYTES = 1 << 30                  # state buffers: units per launch group
 
@@ -181,8 +193,10 @@ class NetPlan:
             ins = sorted(v for v, pi in prod.items() if pi < lo and last.get(v, -1) >= lo)
             outs = sorted(v for v, pi in prod.items() if pi < hi <= last.get(v, -1)) \
                 if hi < len(lowered) else []
-            self.stages.append(self._lower(lowered, lo, hi, np_, ins, outs, last, dual,
-                                           itemsize))
+            st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
+            if np_ == 2 and st.lds_elems * itemsize * 2 > MAX_LDS_BYTES:
+                st = self._lower(lowered, lo, hi, 1, ins, outs, last, dual, itemsize)
+            self.stages.append(st)
         self.need_var = {vf}
         for st in self.stages:
             self.need_var |= {v for _, v in st.records if v is not None}
@@ -261,6 +275,11 @@ class NetPlan:
         for t, (k, pairs) in enumerate(kept):
             hi = kept[t + 1][0] if t + 1 < len(kept) else n
             bounds.append((k, hi, pairs))
+        # the first stage on 2 pairs: two one-pair halves of one workgroup (any op list;
+        # __init__ falls back to 1 when twice the arena does not fit the LDS)
+        lo0, hi0, _ = bounds[0]
+        if first_pairs(len(bounds)) == 2:
+            bounds[0] = (lo0, hi0, 2)
         return bounds
 
     def _lower(self, lowered, lo, hi, pairs, ins, outs, last, dual, itemsize):
@@ -469,7 +488,8 @@ class NetPlan:
                 folded.append((f, v))
             recs = folded
         for f, _ in recs:
-            if f["kind"] == N.CGP_NET_RELU or (f["kind"] == N.CGP_NET_LINEAR and pairs > 1):
+            # (a two-pair stage runs its ops as one-pair halves: lowered like one pair)
+            if f["kind"] == N.CGP_NET_RELU or (f["kind"] == N.CGP_NET_LINEAR and pairs > 2):
                 f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
             elif f["kind"] in (N.CGP_NET_MOMENTS, N.CGP_NET_LINEAR):
                 f["code"] = -1

@@ -36,6 +36,12 @@ namespace {
 #define CGP_NET_NT 128
 #endif
 constexpr int kNT = CGP_NET_NT;  // threads per workgroup (one pair): two waves
+// threads of a workgroup carrying NP pairs: NP == 2 is two one-pair halves on four waves
+// (units u and u + 1, the same image i: the i-side variance loads of the halves meet in
+// L1 and each barrier serves both pairs; net_kernel); the small-map stages pack 4 / 16
+// pairs on two waves.  Ops only ever run on one half (NP = 1) or on NP = 4 / 16.
+template <int NP>
+constexpr int kNTof = NP == 2 ? 2 * kNT : kNT;
 #ifndef CGP_NET_STL
 #define CGP_NET_STL 3
 #endif
@@ -45,13 +51,13 @@ constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
 
 // R | len outputs per item, chosen to minimise rounds·(per-item cost) with ≤ 8 outputs
 // (register budget); ties go to the larger R (fewer LDS reads per output).
-constexpr int pick_r(int lines, int len, int taps, int s, int epi) {
+constexpr int pick_r(int lines, int len, int taps, int s, int epi, int nt) {
     int best = 1;
     long long best_cost = LLONG_MAX;
     for (int r = 1; r <= 8 && r <= len; ++r) {
         if (len % r) continue;
         const int items = lines * (len / r);
-        const int rounds = (items + kNT - 1) / kNT;
+        const int rounds = (items + nt - 1) / nt;
         const long long cost = (long long)rounds * (epi * r + (r - 1) * s + taps);
         if (cost < best_cost || (cost == best_cost && r > best)) {
             best = r;
@@ -66,6 +72,8 @@ template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_, int NP_
 struct NG {
     static constexpr int H = H_, W = W_, HO = HO_, WO = WO_, TAPS = TAPS_, S = S_, OFF = OFF_;
     static constexpr int NP = NP_;
+    static constexpr int NT = kNT;
+    static_assert(NP_ != 2, "two-pair workgroups run their ops as one-pair halves");
     static constexpr int HW = H * W, HOWO = HO * WO;
     static constexpr bool POINT = TAPS == 1 && OFF == 0;
     static constexpr bool REDUCE = HO == 1 && WO == 1 && OFF == 0 && TAPS == H && TAPS == W;
@@ -73,11 +81,11 @@ struct NG {
     static constexpr int Q0 = OFF < 0 ? -OFF : 0;              // first hs row backed by input
     static constexpr int Q1 = HSR < H - OFF ? HSR : H - OFF;   // one past the last
     static constexpr int NVR = Q1 - Q0;                        // input rows the row pass reads
-    static constexpr int R2 = pick_r(NVR * NP, WO, TAPS, S, 2);
-    static constexpr int R3 = pick_r(WO * NP, HO, TAPS, S, 8);
+    static constexpr int R2 = pick_r(NVR * NP, WO, TAPS, S, 2, NT);
+    static constexpr int R3 = pick_r(WO * NP, HO, TAPS, S, 8, NT);
     static constexpr int WIN2 = (R2 - 1) * S + TAPS, WIN3 = (R3 - 1) * S + TAPS;
-    static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NP * NH + kNT - 1) / kNT;
-    static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NP * NV + kNT - 1) / kNT;
+    static constexpr int NG2 = WO / R2, NH = NVR * NG2, KH = (NP * NH + NT - 1) / NT;
+    static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NP * NV + NT - 1) / NT;
     static constexpr int NZ = (HSR - NVR) * WO;                // zero cells of hs
     // windows of at most 3 taps (the ResNets' 3x3 convs) run in one pass straight from the
     // source slot: no row-sum scratch, so a smaller arena (CGP_NET_DIRECT=0: separable)
@@ -177,9 +185,11 @@ __device__ __forceinline__ void win_sums(const T (&w)[(R - 1) * S + TAPS], T (&o
 // threadIdx.x through an opaque move: per-thread index math of one op is then recomputed
 // inside the op instead of being hoisted out of the pair loop, where it would hold
 // registers for every geometry at once
+// (thread index within its 128-thread half: a two-pair workgroup runs one pair per half)
 __device__ __forceinline__ int opaque_tid() {
+    static_assert(kNT == 128, "opaque_tid masks to 128-thread halves");
     int t;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    asm volatile("v_and_b32 %0, 0x7f, %1" : "=v"(t) : "v"((int)threadIdx.x));
     return t;
 }
 
@@ -345,21 +355,60 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
     }
 }
 
-// variances for the op's ReLU (var_x/var_y) or its dst2 ReLU (var2_x/var2_y)
+// A pointer every lane holds the same value of (an op-record field) as a scalar: loads
+// through it take the SGPR-base form (global_load … vOFF, s[BASE] offset:IMM), so a
+// variance load costs no 64-bit VALU address arithmetic
+__device__ __forceinline__ GP<char> ubase(const void* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (GP<char>)(const char*)(((unsigned long long)hi << 32) | lo);
+}
+
+// variances for the op's ReLU (var_x/var_y) or its dst2 ReLU (var2_x/var2_y).  x / y are
+// uniform bases; xo / yo the byte offsets of the pair's maps when they differ per lane
+// (multi-pair stages), else 0 with the image offset folded into the base.  ldx(px, k)
+// reads pixel px + k of the x-side map: px is the per-lane part (one 32-bit offset
+// register shared by both sides when the offsets are folded), k a compile-time step
+// that lands in the instruction's immediate offset.  Per-lane offsets are 32-bit: the
+// multi-pair maps are at most 32x32, and net_impl bounds n1, n2 so they cannot wrap.
 template <typename T>
 struct VarSrc {
-    GP<T> x, y;
+    GP<char> x, y;
+    unsigned xo, yo;
     bool on;
+    __device__ __forceinline__ T ldx(unsigned px, int k = 0) const {
+        return *(GP<T>)(x + (size_t)(xo + px * (unsigned)sizeof(T)) + k * (int)sizeof(T));
+    }
+    __device__ __forceinline__ T ldy(unsigned px, int k = 0) const {
+        return *(GP<T>)(y + (size_t)(yo + px * (unsigned)sizeof(T)) + k * (int)sizeof(T));
+    }
 };
-template <typename T>
+// UNI: i and j are the same in every lane (one pair per workgroup), so their offsets fold
+// into the scalar bases
+template <typename T, bool UNI>
+__device__ __forceinline__ VarSrc<T> var_maps(const void* vx, const void* vy, bool on,
+                                              unsigned i, unsigned j, int hw) {
+    VarSrc<T> r;
+    r.on = on;
+    r.x = ubase(vx);
+    r.y = ubase(vy);
+    if constexpr (UNI) {
+        r.x += (size_t)i * (size_t)hw * sizeof(T);   // scalar 64-bit arithmetic
+        r.y += (size_t)j * (size_t)hw * sizeof(T);
+        r.xo = r.yo = 0;
+    } else {
+        r.xo = i * (unsigned)hw * (unsigned)sizeof(T);
+        r.yo = j * (unsigned)hw * (unsigned)sizeof(T);
+    }
+    return r;
+}
+template <typename T, bool UNI>
 __device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, unsigned j,
                                              int hw) {
     const bool two = op.dst2 >= 0;
-    VarSrc<T> r;
-    r.on = op.relu != 0 || two;
-    r.x = gptr<T>(two ? op.var2_x : op.var_x) + (size_t)i * hw;
-    r.y = gptr<T>(two ? op.var2_y : op.var_y) + (size_t)j * hw;
-    return r;
+    return var_maps<T, UNI>(two ? op.var2_x : op.var_x, two ? op.var2_y : op.var_y,
+                            op.relu != 0 || two, i, j, hw);
 }
 
 // ---- CGP_NET_CONV -------------------------------------------------------------------
@@ -375,14 +424,14 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
-    const VarSrc<T> vs0 = var_src<T>(op, pr.i, pr.j, G::HOWO);   // NP == 1
+    const VarSrc<T> vs0 = var_src<T, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
         if constexpr (NP == 1) {
             return vs0;
         } else {
             unsigned iq, jq;
             pair_q<NP>(pr, q, iq, jq);
-            return var_src<T>(op, iq, jq, G::HOWO);
+            return var_src<T, false>(op, iq, jq, G::HOWO);
         }
     };
     const T* __restrict__ src = lds + op.src;
@@ -392,9 +441,9 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // 1x1 output from a full-plane window: a block reduction
         T acc = T(0);
 #pragma unroll
-        for (int k = 0; k < (G::HW + kNT - 1) / kNT; ++k) {
-            const int px = tid + k * kNT;
-            if (G::HW % kNT == 0 || px < G::HW) {
+        for (int k = 0; k < (G::HW + G::NT - 1) / G::NT; ++k) {
+            const int px = tid + k * G::NT;
+            if (G::HW % G::NT == 0 || px < G::HW) {
                 const int r = udiv(px, G::W), c = px - r * G::W;
                 acc += src[r * wsi + c];
             }
@@ -406,22 +455,22 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if (tid == 0) {
             T tot = part[0];
 #pragma unroll
-            for (int k = 1; k < kNT / 64; ++k) tot += part[k];
+            for (int k = 1; k < G::NT / 64; ++k) tot += part[k];
             T v[1] = {fma_t(w, tot, b)};
             const int at[1] = {0};
             const bool ok[1] = {true};
             T u1[1] = {T(1)}, u2[1] = {T(1)};
             if (vs0.on) {
-                u1[0] = vs0.x[0];
-                u2[0] = vs0.y[0];
+                u1[0] = vs0.ldx(0);
+                u2[0] = vs0.ldy(0);
             }
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::REDUCE) {
-        // NP pairs: kNT / NP lanes per pair (within one wave) sum its map, then a
+        // NP pairs: G::NT / NP lanes per pair (within one wave) sum its map, then a
         // segmented butterfly; the group's first lane finishes the pair
-        constexpr int TPP = kNT / NP;
-        static_assert(TPP <= 64 && kNT % NP == 0, "reduce groups must not straddle waves");
+        constexpr int TPP = G::NT / NP;
+        static_assert(TPP <= 64 && G::NT % NP == 0, "reduce groups must not straddle waves");
         const int q = udiv(tid, TPP), lane = tid - q * TPP;
         const T* srcq = src + q * arena;
         T acc = T(0);
@@ -442,28 +491,28 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             const bool ok[1] = {true};
             T u1[1] = {T(1)}, u2[1] = {T(1)};
             if (vs.on) {
-                u1[0] = vs.x[0];
-                u2[0] = vs.y[0];
+                u1[0] = vs.ldx(0);
+                u2[0] = vs.ldy(0);
             }
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::POINT) {
         constexpr int N = NP * G::HOWO;
-        constexpr int KP = (N + kNT - 1) / kNT;
+        constexpr int KP = (N + G::NT - 1) / G::NT;
         T u1[KP], u2[KP], v[KP];
         int at[KP];
         bool ok[KP];
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
-            const int e = tid + k * kNT;
-            ok[k] = N % kNT == 0 || e < N;
+            const int e = tid + k * G::NT;
+            ok[k] = N % G::NT == 0 || e < N;
             const int ec = ok[k] ? e : 0;
             const int q = NP == 1 ? 0 : udiv(ec, G::HOWO), pc = ec - q * G::HOWO;
             const int r = udiv(pc, G::WO), c = pc - r * G::WO;
             const VarSrc<T> vs = vs_of(q);
             at[k] = q * arena + r * wso + c;
-            u1[k] = (vs.on && ok[k]) ? vs.x[(unsigned)pc] : T(1);
-            u2[k] = (vs.on && ok[k]) ? vs.y[(unsigned)pc] : T(1);
+            u1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : T(1);
+            u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
         net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
@@ -476,15 +525,16 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         T u1[G::KV][G::R3], u2[G::KV][G::R3];
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
-            const int it = tid + kv * kNT;
-            const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
+            const int it = tid + kv * G::NT;
+            const int itc = (NVT % G::NT == 0 || it < NVT) ? it : 0;
             const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
             const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
             const VarSrc<T> vs = vs_of(q);
 #pragma unroll
             for (int k = 0; k < G::R3; ++k) {
-                u1[kv][k] = vs.on ? vs.x[(unsigned)((g3 * G::R3 + k) * G::WO + c)] : T(1);
-                u2[kv][k] = vs.on ? vs.y[(unsigned)((g3 * G::R3 + k) * G::WO + c)] : T(1);
+                const unsigned px0 = (unsigned)(g3 * G::R3 * G::WO + c);
+                u1[kv][k] = vs.on ? vs.ldx(px0, k * G::WO) : T(1);
+                u2[kv][k] = vs.on ? vs.ldy(px0, k * G::WO) : T(1);
             }
         }
         // outputs that land on the source (in place, or dst2 on the source) are stored
@@ -497,8 +547,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         T res[G::KV][G::R3];
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
-            const int it = tid + kv * kNT;
-            if (NVT % kNT == 0 || it < NVT) {
+            const int it = tid + kv * G::NT;
+            if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const T* base = src + q * arena + c * G::S + G::OFF;
@@ -527,8 +577,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if (hazard) lds_barrier();
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
-            const int it = tid + kv * kNT;
-            if (NVT % kNT == 0 || it < NVT) {
+            const int it = tid + kv * G::NT;
+            if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 int at[G::R3];
@@ -549,15 +599,16 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         if (vs0.on) {
 #pragma unroll
             for (int kv = 0; kv < G::KV; ++kv) {
-                const int it = tid + kv * kNT;
-                const int itc = (NVT % kNT == 0 || it < NVT) ? it : 0;
+                const int it = tid + kv * G::NT;
+                const int itc = (NVT % G::NT == 0 || it < NVT) ? it : 0;
                 const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const VarSrc<T> vs = vs_of(q);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
-                    u1[kv][k] = vs.x[(unsigned)((g3 * G::R3 + k) * G::WO + c)];
-                    u2[kv][k] = vs.y[(unsigned)((g3 * G::R3 + k) * G::WO + c)];
+                    const unsigned px0 = (unsigned)(g3 * G::R3 * G::WO + c);
+                    u1[kv][k] = vs.ldx(px0, k * G::WO);
+                    u2[kv][k] = vs.ldy(px0, k * G::WO);
                 }
             }
         } else {
@@ -569,8 +620,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
 #pragma unroll
         for (int kh = 0; kh < G::KH; ++kh) {
-            const int it = tid + kh * kNT;
-            if (NHT % kNT == 0 || it < NHT) {
+            const int it = tid + kh * G::NT;
+            if (NHT % G::NT == 0 || it < NHT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NH), l = it - q * G::NH;
                 const int qi = udiv(l, G::NG2), g2 = l - qi * G::NG2;
                 const T* row = src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
@@ -588,9 +639,9 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // hs rows outside the input are zero (the scratch is shared by every conv)
         if constexpr (G::NZ > 0) {
 #pragma unroll
-            for (int z0 = 0; z0 < NZT; z0 += kNT) {
+            for (int z0 = 0; z0 < NZT; z0 += G::NT) {
                 const int z = z0 + tid;
-                if (NZT % kNT == 0 || z < NZT) {
+                if (NZT % G::NT == 0 || z < NZT) {
                     const int q = NP == 1 ? 0 : udiv(z, G::NZ), zl = z - q * G::NZ;
                     hs[q * arena + (zl < G::Q0 * G::WO ? zl : zl + G::NVR * G::WO)] = T(0);
                 }
@@ -601,8 +652,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // stage is one basic block, so the R3 independent ReLUs interleave)
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
-            const int it = tid + kv * kNT;
-            if (NVT % kNT == 0 || it < NVT) {
+            const int it = tid + kv * G::NT;
+            if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
                 const T* col = hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
@@ -631,7 +682,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 }
 
 // ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
-// One pass: KE pixels per thread at e = base + k·kNT + tid over the NP pairs' maps
+// One pass: KE pixels per thread at e = base + k·NT + tid over the NP pairs' maps
 // (pair q = e / hw; NP > 1 needs the compile-time size W_).
 template <typename T, bool EX, bool DU, int KIND, int KE, int W_, int NP>
 __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op& op,
@@ -644,9 +695,9 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     // RELU reads (var_x, var_y) = variances of src (an elementwise ReLU has no dst2);
     // LINEAR may carry a dst2 ReLU with (var2_x, var2_y)
     auto vs_of = [&](unsigned iq, unsigned jq) {
-        return KIND == CGP_NET_RELU ? VarSrc<T>{gptr<T>(op.var_x) + (size_t)iq * hw,
-                                                gptr<T>(op.var_y) + (size_t)jq * hw, true}
-                                    : var_src<T>(op, iq, jq, hw);
+        return KIND == CGP_NET_RELU
+                   ? var_maps<T, NP == 1>(op.var_x, op.var_y, true, iq, jq, hw)
+                   : var_src<T, NP == 1>(op, iq, jq, hw);
     };
     const VarSrc<T> vs0 = vs_of(pr.i, pr.j);
     const GP<T> xi = gptr<T>(p.x) + (size_t)pr.i * p.channels * hw;
@@ -671,17 +722,26 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             pair_q<NP>(pr, q, iq, jq);
             vs = vs_of(iq, jq);
         }
-        u1[k] = (vs.on && ok[k]) ? vs.x[(unsigned)pc] : T(1);
-        u2[k] = (vs.on && ok[k]) ? vs.y[(unsigned)pc] : T(1);
+        u1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : T(1);
+        u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
         if constexpr (KIND == CGP_NET_RELU) {
             a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
+            static_assert(NP == 1, "moments run one pair per workgroup (half)");
             T acc = xi[pc] * yj[pc];
             for (int ch = 1; ch < p.channels; ++ch)
                 acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
-            a[k] = p.channels == 1 ? acc : acc / T(p.channels);   // x / 1 == x
+            a[k] = acc;
         } else {
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
+        }
+    }
+    if constexpr (KIND == CGP_NET_MOMENTS) {
+        // the channel mean (x / 1 == x: a uniform branch, so one-channel inputs run no
+        // division at all)
+        if (p.channels != 1) {
+#pragma unroll
+            for (int k = 0; k < KE; ++k) a[k] = a[k] / T(p.channels);
         }
     }
     if constexpr (KIND == CGP_NET_RELU) {
@@ -760,12 +820,12 @@ __device__ __forceinline__ void net_move(T* __restrict__ lds, const cgp_net_op& 
 // Zero the halo cells of the slot whose pixel (0, 0) is at `origin` (code = (HL << 8) |
 // gap, see cgp_net_op.zero_halo): HL cells before it and `gap` after each of the h rows.
 // Disjoint from every data cell, so it needs no barrier against the op's own writes.
-template <typename T>
+template <typename T, int NT>
 __device__ __forceinline__ void zero_halos(T* lds, int origin, int code, int h, int w, int ws,
                                            int tid) {
     if (!code) return;
     const int hl = code >> 8, gap = code & 0xff;
-    for (int e = tid; e < hl + h * gap; e += kNT) {
+    for (int e = tid; e < hl + h * gap; e += NT) {
         int cell;
         if (e < hl) {
             cell = origin - hl + e;
@@ -858,8 +918,9 @@ __device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
             const int qa = NP == 1 ? 0 : q * p.lds_elems;
-            zero_halos(lds + qa, op.dst, op.zero_halo & 0xffff, op.h, op.w, op.ws_out, tid);
-            zero_halos(lds + qa, op.dst2, (unsigned)op.zero_halo >> 16, op.h, op.w,
+            zero_halos<T, kNT>(lds + qa, op.dst, op.zero_halo & 0xffff, op.h, op.w,
+                                     op.ws_out, tid);
+            zero_halos<T, kNT>(lds + qa, op.dst2, (unsigned)op.zero_halo >> 16, op.h, op.w,
                        op.ws_out, tid);
         }
     }
@@ -937,8 +998,10 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 const int qa = q * I.lds_elems;
-                zero_halos(lds + qa, o.dst, o.zero_halo & 0xffff, o.h, o.w, o.ws_out, tid);
-                zero_halos(lds + qa, o.dst2, (unsigned)o.zero_halo >> 16, o.h, o.w, o.ws_out,
+                zero_halos<T, kNT>(lds + qa, o.dst, o.zero_halo & 0xffff, o.h, o.w,
+                                         o.ws_out, tid);
+                zero_halos<T, kNT>(lds + qa, o.dst2, (unsigned)o.zero_halo >> 16, o.h, o.w,
+                                         o.ws_out,
                            tid);
             }
         }
@@ -983,18 +1046,19 @@ int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_ele
 // WPE: waves per SIMD the register allocation targets (amdgpu_waves_per_eu).  LDS caps
 // the resident workgroups per CU (two waves each) at 160 KB / footprint, so allocating
 // registers for more waves than that only forces spills; net_launch picks WPE from the
-// LDS footprint (net_wpe).  NP: pairs per workgroup (1, or 4 / 16 for small-map stages).
+// LDS footprint (net_wpe).  NP: pairs per workgroup (1; 2 on four waves, sharing image i;
+// 4 / 16 for small-map stages).
 #ifndef CGP_NET_DYN
 #define CGP_NET_DYN 1
 #endif
 // PID >= 0: compiled program PID instead of the op-record interpreter.
 template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
+__global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     __shared__ unsigned pair_tab[2 * kMaxNP];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
-    for (int e = tid; e < NP * p.lds_elems; e += kNT) lds[e] = T(0);   // slot halos stay zero
+    for (int e = tid; e < NP * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
     lds_barrier();
     // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
     // contiguous run of supertiles and its L2 holds the images/variances they share.
@@ -1033,50 +1097,100 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
-        if constexpr (NP == 1) {
-            if (!unit_pair(p, u, pr.i, pr.j)) continue;
-            if (p.same && pr.j <= pr.i) {
-                if (p.final_stage && pr.j == pr.i && tid == 0)
-                    p.out[(long long)pr.i * p.ldo + pr.i] = p.kdiag[pr.i];
+        if constexpr (NP == 2) {
+            // two one-pair halves sharing the workgroup's barriers: waves 0-1 run unit u,
+            // waves 2-3 unit u + 1 (the next j of the same image i), each on its own
+            // arena.  Every wave decodes both units (scalar), so the pair is uniform per
+            // wave and each half runs the one-pair code (scalar variance-map bases)
+            unsigned i0, j0, i1 = 0, j1 = 0;
+            const bool v0 = unit_pair(p, u, i0, j0);
+            const bool v1 = u + 1 < end && unit_pair(p, u + 1, i1, j1);
+            const bool w0 = v0 && !(p.same && j0 <= i0), w1 = v1 && !(p.same && j1 <= i1);
+            if (!w0 && !w1) {   // both below the diagonal of a same tile (or outside)
+                if (p.final_stage && p.same && tid == 0) {
+                    if (v0 && j0 == i0) p.out[(long long)i0 * p.ldo + i0] = p.kdiag[i0];
+                    if (v1 && j1 == i1) p.out[(long long)i1 * p.ldo + i1] = p.kdiag[i1];
+                }
                 continue;
             }
-        } else {
-            // the group's pair table; pairs outside the tile are computed on clamped
-            // indices and never stored
-            if (tid < NP) {
-                unsigned iq = 0, jq = 0;
-                unit_pair(p, u + tid, iq, jq);
-                pair_tab[tid] = iq < p.n1 ? iq : p.n1 - 1;
-                pair_tab[kMaxNP + tid] = jq < p.n2 ? jq : p.n2 - 1;
+            const int q = __builtin_amdgcn_readfirstlane(tid >> 7);
+            const bool vq = q ? v1 : v0, wq = q ? w1 : w0;
+            Pairs ph;
+            ph.tab = pair_tab;
+            ph.u0 = u + q;
+            // a half without a pair computes on clamped indices and stores nothing
+            ph.i = vq ? (q ? i1 : i0) : 0u;
+            ph.j = vq ? (q ? j1 : j0) : 0u;
+            ph.i = __builtin_amdgcn_readfirstlane(ph.i);
+            ph.j = __builtin_amdgcn_readfirstlane(ph.j);
+            T* lh = lds + q * p.lds_elems;
+            const int ht = tid & (kNT - 1);
+            if constexpr (PID < 0) {
+                for (int k = 0; k < p.nops; ++k) {
+                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
+                    net_op<T, EX, DU, 1>(lh, op, p, ph, ht);
+                    lds_barrier();
+                }
+            } else {
+                prog_ops<T, DU, 1, PID, 0>(lh, p, ph, ht);
             }
-            pr.i = pr.j = 0;
-            lds_barrier();
-        }
-        if constexpr (PID < 0) {
-            for (int k = 0; k < p.nops; ++k) {
-                const cgp_net_op op = load_op(ops_c(p.ops) + k);
-                net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
+            if (p.final_stage && ht == 0 && vq) {
+                if (wq) {
+                    const T v = lh[p.final_slot];
+                    p.out[(long long)ph.i * p.ldo + ph.j] = v;
+                    if (p.same) p.out[(long long)ph.j * p.ldo + ph.i] = v;
+                } else if (ph.j == ph.i) {
+                    p.out[(long long)ph.i * p.ldo + ph.i] = p.kdiag[ph.i];
+                }
+            }
+        } else {
+            if constexpr (NP == 1) {
+                if (!unit_pair(p, u, pr.i, pr.j)) continue;
+                pr.i = __builtin_amdgcn_readfirstlane(pr.i);   // uniform: scalar map offsets
+                pr.j = __builtin_amdgcn_readfirstlane(pr.j);
+                if (p.same && pr.j <= pr.i) {
+                    if (p.final_stage && pr.j == pr.i && tid == 0)
+                        p.out[(long long)pr.i * p.ldo + pr.i] = p.kdiag[pr.i];
+                    continue;
+                }
+            } else {
+                // the group's pair table; pairs outside the tile are computed on clamped
+                // indices and never stored
+                if (tid < NP) {
+                    unsigned iq = 0, jq = 0;
+                    unit_pair(p, u + tid, iq, jq);
+                    pair_tab[tid] = iq < p.n1 ? iq : p.n1 - 1;
+                    pair_tab[kMaxNP + tid] = jq < p.n2 ? jq : p.n2 - 1;
+                }
+                pr.i = pr.j = 0;
                 lds_barrier();
             }
-        } else {
-            prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid);
-        }
-        if (p.final_stage) {
-            if constexpr (NP == 1) {
-                if (tid == 0) {
-                    const T v = lds[p.final_slot];
-                    p.out[(long long)pr.i * p.ldo + pr.j] = v;
-                    if (p.same) p.out[(long long)pr.j * p.ldo + pr.i] = v;
+            if constexpr (PID < 0) {
+                for (int k = 0; k < p.nops; ++k) {
+                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
+                    net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
+                    lds_barrier();
                 }
-            } else if (tid < NP) {
-                unsigned iq, jq;
-                if (u + tid < end && unit_pair(p, u + tid, iq, jq)) {
-                    if (!p.same || jq > iq) {
-                        const T v = lds[tid * p.lds_elems + p.final_slot];
-                        p.out[(long long)iq * p.ldo + jq] = v;
-                        if (p.same) p.out[(long long)jq * p.ldo + iq] = v;
-                    } else if (jq == iq) {
-                        p.out[(long long)iq * p.ldo + iq] = p.kdiag[iq];
+            } else {
+                prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid);
+            }
+            if (p.final_stage) {
+                if constexpr (NP == 1) {
+                    if (tid == 0) {
+                        const T v = lds[p.final_slot];
+                        p.out[(long long)pr.i * p.ldo + pr.j] = v;
+                        if (p.same) p.out[(long long)pr.j * p.ldo + pr.i] = v;
+                    }
+                } else if (tid < NP) {
+                    unsigned iq, jq;
+                    if (u + tid < end && unit_pair(p, u + tid, iq, jq)) {
+                        if (!p.same || jq > iq) {
+                            const T v = lds[tid * p.lds_elems + p.final_slot];
+                            p.out[(long long)iq * p.ldo + jq] = v;
+                            if (p.same) p.out[(long long)jq * p.ldo + iq] = v;
+                        } else if (jq == iq) {
+                            p.out[(long long)iq * p.ldo + iq] = p.kdiag[iq];
+                        }
                     }
                 }
             }
@@ -1085,11 +1199,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-// waves per SIMD the LDS footprint allows (kNT / 64 waves per workgroup, 4 SIMDs per CU),
-// clamped to the instantiated register targets 3..5
-constexpr int net_wpe(long long lds_bytes, int cap = 5) {
+// waves per SIMD the LDS footprint of a workgroup allows (`waves` waves per workgroup,
+// 4 SIMDs per CU), clamped to the instantiated register targets 3..5
+constexpr int net_wpe(long long lds_bytes, int cap = 5, int waves = kNT / 64) {
     const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
-    const long long w = wg * (kNT / 64) / 4;
+    const long long w = wg * waves / 4;
     return w < 3 ? 3 : (w > cap ? cap : (int)w);
 }
 #ifndef CGP_NET_PROG_WPE_MAX
@@ -1101,7 +1215,7 @@ constexpr int net_wpe(long long lds_bytes, int cap = 5) {
 // (DU, pairs); the exact ReLU runs one pair per workgroup
 template <typename T, int NP>
 const void* net_fn_np(bool du, long long lds_bytes) {
-    switch (net_wpe(lds_bytes)) {
+    switch (net_wpe(lds_bytes, 5, kNTof<NP> / 64)) {
     case 3: return du ? (const void*)net_kernel<T, false, true, 3, NP>
                       : (const void*)net_kernel<T, false, false, 3, NP>;
     case 4: return du ? (const void*)net_kernel<T, false, true, 4, NP>
@@ -1121,6 +1235,7 @@ const void* net_fn(bool ex, bool du, int np, long long lds_bytes) {
     if constexpr (sizeof(T) == 8) {
         switch (np) {
         case 1: return net_fn_np<T, 1>(du, lds_bytes);
+        case 2: return net_fn_np<T, 2>(du, lds_bytes);
         case 4: return net_fn_np<T, 4>(du, lds_bytes);
         case 16: return net_fn_np<T, 16>(du, lds_bytes);
         default: return nullptr;
@@ -1130,6 +1245,8 @@ const void* net_fn(bool ex, bool du, int np, long long lds_bytes) {
     switch (np) {
     case 1: return du ? (const void*)net_kernel<T, false, true, 4, 1>
                       : (const void*)net_kernel<T, false, false, 5, 1>;
+    case 2: return du ? (const void*)net_kernel<T, false, true, 4, 2>
+                      : (const void*)net_kernel<T, false, false, 5, 2>;
     case 4: return du ? (const void*)net_kernel<T, false, true, 4, 4>
                       : (const void*)net_kernel<T, false, false, 5, 4>;
     case 16: return du ? (const void*)net_kernel<T, false, true, 4, 16>
@@ -1146,7 +1263,9 @@ const void* prog_fn_one() {
         return nullptr;
     } else {
         constexpr long long bytes = (long long)I.lds_elems * (long long)sizeof(T) * I.pairs;
-        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX) : (I.dual ? 4 : 5);
+        constexpr int wpe = sizeof(T) == 8
+                                ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX, (I.pairs == 2 ? 2 * kNT : kNT) / 64)
+                                : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
 }
@@ -1161,7 +1280,10 @@ const void* prog_fn(int pid) {
     }
 }
 
-int net_occupancy(const void* fn, int lds_bytes) {
+// threads of a workgroup of np pairs (kNTof at run time)
+int net_threads(int np) { return np == 2 ? kNTof<2> : kNT; }
+
+int net_occupancy(const void* fn, int lds_bytes, int threads) {
     if (lds_bytes > 64 * 1024 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
             hipSuccess) {
@@ -1169,7 +1291,7 @@ int net_occupancy(const void* fn, int lds_bytes) {
         return 0;
     }
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kNT, lds_bytes) != hipSuccess) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds_bytes) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
@@ -1180,7 +1302,7 @@ template <typename T>
 int net_occupancy_for(int lds_bytes, int flags, int np) {
     const void* fn = net_fn<T>(flags & CGP_FLAG_EXACT_RELU, flags & CGP_FLAG_NET_DUAL, np,
                                (long long)lds_bytes * np);
-    return fn ? net_occupancy(fn, lds_bytes * np) : 0;
+    return fn ? net_occupancy(fn, lds_bytes * np, net_threads(np)) : 0;
 }
 
 // Per-XCD unit counters for a launch: 8 × u64 slots of a 64-slot ring owned by the launch
@@ -1236,7 +1358,7 @@ int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, 
     const long long wg_bytes = lds_bytes * np;
     const void* fn = program > 0 && !ex ? prog_fn<T>(program - 1) : net_fn<T>(ex, du, np, wg_bytes);
     if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
-    const int per_cu = net_occupancy(fn, (int)wg_bytes);
+    const int per_cu = net_occupancy(fn, (int)wg_bytes, net_threads(np));
     if (per_cu <= 0)
         return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", wg_bytes);
     const long long groups = (p.uend - p.ubeg + np - 1) / np;
@@ -1248,7 +1370,7 @@ int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, 
     arg.work = work_counters(s);
     if (!arg.work) return fail(CGP_EHIP, "net: work counters");
     void* args[] = {&arg};
-    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kNT), args,
+    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(net_threads(np)), args,
                                          (size_t)wg_bytes, s);
     if (e != hipSuccess) return fail(CGP_EHIP, "net_kernel launch: %s", hipGetErrorString(e));
     return check_launch("net_kernel");
@@ -1297,10 +1419,16 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
     const int np = a->pairs <= 0 ? 1 : a->pairs;
-    if (np != 1 && np != 4 && np != kMaxNP)
-        return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 4 or 16)", np);
+    if (np != 1 && np != 2 && np != 4 && np != kMaxNP)
+        return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 2, 4 or 16)", np);
     if (lds_bytes * np > 160 * 1024)
         return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * np);
+    // multi-pair stages address a pair's variance maps (<= 8 * threads / np pixels) with
+    // 32-bit byte offsets (VarSrc)
+    if (np > 1 && (a->n1 > a->n2 ? a->n1 : a->n2) * (8LL * net_threads(np) / np) *
+                          (long long)sizeof(T) >= (1LL << 32))
+        return fail(CGP_EINVAL, "net: %lld images too many for %d pairs per workgroup",
+                    (long long)(a->n1 > a->n2 ? a->n1 : a->n2), np);
     if (a->unit_begin == 0 && a->unit_end == 0) {
         p.ubeg = 0;
         p.uend = p.units;

@@ -382,13 +382,16 @@ def test_netfuse_ragged_tiles_vs_oracle(n1, n2):
 
 @pytest.mark.parametrize("cfg", ["mnist_as_tf", "cifar10"])
 @pytest.mark.parametrize("same", [False, True])
-def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, monkeypatch):
-    """multi-pair stages (4 / 16 pairs per workgroup on the 14x14 / 7x7 tail) against the
-    one-stage program and the oracle, with the state buffers chunked to 64 units per
-    launch group so every launch carries a unit range and a range-relative state index"""
+@pytest.mark.parametrize("first", ["1", "2"])
+def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, first, monkeypatch):
+    """multi-pair stages (4 / 16 pairs per workgroup on the 14x14 / 7x7 tail; the 28x28 /
+    32x32 head on 1 or 2 pairs) against the one-stage program and the oracle, with the
+    state buffers chunked to 64 units per launch group so every launch carries a unit
+    range and a range-relative state index"""
     from cnn_gp import netplan
     from cnn_gp.program import Plan
     monkeypatch.setattr(netplan, "CHUNK_BYTES", 64 * 8 * 512)
+    monkeypatch.setattr(netplan, "FIRST_PAIRS", first)
     C, side = specs.GEOMETRY[cfg]
     rng = np.random.default_rng(31)
     X = rng.random((21, C, side, side))
@@ -397,7 +400,7 @@ def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, monkeypatch):
     plan = m._plan(side, side)
     multi = netplan.NetPlan(plan, 8)
     single = netplan.NetPlan(plan, 8, stages=False)
-    assert [st.pairs for st in multi.stages] == [1, 4, 16]
+    assert [st.pairs for st in multi.stages] == [netplan.first_pairs(3), 4, 16]
     assert len(single.stages) == 1
     x, z = dev(X), dev(Z)
     n1, n2 = len(X), len(Z)
@@ -415,6 +418,32 @@ def test_netfuse_stages_match_single_stage_and_oracle(cfg, same, monkeypatch):
     if same:                                   # the kernel fills both triangles
         assert np.array_equal(a, a.T)
     assert rel_err(a, ref) < RTOL64["fast"]
+
+
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp",
+                                 "mnist_as_tf", "cifar10"])
+@pytest.mark.parametrize("same", [False, True])
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_first_stage_pairs_bit_equal(cfg, same, dt, monkeypatch):
+    """the head stage on 2 pairs per workgroup (four waves, pairs u and u+1 sharing the
+    walk's image i) and on 1 pair run each pair through the same arithmetic: bit-equal
+    tiles, ragged sizes so groups straddle rows and the tile edge"""
+    from cnn_gp import netplan
+    C, side = specs.GEOMETRY[cfg]
+    rng = np.random.default_rng(7)
+    X = rng.random((13, C, side, side))
+    Z = X if same else rng.random((11, C, side, side))
+    out = {}
+    for first in ("1", "2"):
+        monkeypatch.setattr(netplan, "FIRST_PAIRS", first)
+        m = configs_util.model(cfg).to(DEV, dt)          # fresh model: no cached plan
+        net = m._net_plan(m._plan(side, side), torch.empty((), dtype=dt).element_size())
+        assert net is not None and net.stages[0].pairs == int(first)
+        with torch.no_grad():
+            x = torch.from_numpy(X).to(DEV, dt)
+            out[first] = (m(x) if same else
+                          m(x, torch.from_numpy(Z).to(DEV, dt), False, False)).cpu().numpy()
+    assert np.array_equal(out["1"], out["2"], equal_nan=True)
 
 
 @pytest.mark.parametrize("net", ["big", "small"])

@@ -397,17 +397,18 @@ def test_program_match_ignores_weights_but_not_structure():
     var = {v: (dummy, dummy) for v in net.need_var}
     arr = net._ops_array(st, var)
     lib = N.load()
-    pid = lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8)
+    np_ = st.pairs
+    pid = lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, 0, st.lds_elems, 8)
     assert pid > 0
     for o in arr:
         o.weight, o.bias = 3.5, 0.25
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8) == pid
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, 0, st.lds_elems, 8) == pid
     arr[3].dst += 1
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, 0, st.lds_elems, 8) == 0
     arr[3].dst -= 1
     # other pair count, dual flag, footprint or item size: no program
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 4, 0, st.lds_elems, 8) == 0
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, N.CGP_FLAG_NET_DUAL,
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 4 if np_ != 4 else 1, 0, st.lds_elems, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, N.CGP_FLAG_NET_DUAL,
                                st.lds_elems, 8) == 0
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, 1, 0, st.lds_elems + 2, 8) == 0
-    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops - 1, 1, 0, st.lds_elems, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, 0, st.lds_elems + 2, 8) == 0
+    assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops - 1, np_, 0, st.lds_elems, 8) == 0
