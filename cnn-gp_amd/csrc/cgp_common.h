@@ -161,12 +161,6 @@ __device__ __forceinline__ float fma_t(float a, float b, float c) {
 // pins them in VGPRs and turns every Horner step into v_mov_b64 + v_fmac_f64; read from
 // a __constant__ table through a pointer it cannot hoist (poly_table()), each step is one
 // v_fma_f64 with an SGPR-pair operand and the table lives in SGPRs only while in use.
-static __constant__ double kReluPolyTabD[kReluPolyDegD + 1] = {
-#define CGP_C(k) kReluPolyD[k]
-    CGP_C(0), CGP_C(1), CGP_C(2), CGP_C(3), CGP_C(4), CGP_C(5), CGP_C(6), CGP_C(7),
-    CGP_C(8), CGP_C(9), CGP_C(10), CGP_C(11), CGP_C(12), CGP_C(13)};
-#undef CGP_C
-static_assert(kReluPolyDegD == 13, "kReluPolyTabD lists 14 coefficients");
 // P̃(x4) = P(x4/4)/16: coefficient k scaled by 1/(16·4^k), exact powers of two, so Horner in
 // x4 = 4x rounds exactly like Horner in x (relu_q_n)
 constexpr double poly_q(int k) {
@@ -174,17 +168,24 @@ constexpr double poly_q(int k) {
     for (int n = 0; n < k; ++n) v *= 0.25;
     return v;
 }
-static __constant__ double kReluPolyTabDq[kReluPolyDegD + 1] = {
-    poly_q(0), poly_q(1), poly_q(2), poly_q(3), poly_q(4), poly_q(5), poly_q(6),
-    poly_q(7), poly_q(8), poly_q(9), poly_q(10), poly_q(11), poly_q(12), poly_q(13)};
+struct PolyCoef {
+    double c[kReluPolyDegD + 1];
+};
+constexpr PolyCoef poly_coef(bool quartered) {
+    PolyCoef t{};
+    for (int k = 0; k <= kReluPolyDegD; ++k) t.c[k] = quartered ? poly_q(k) : kReluPolyD[k];
+    return t;
+}
+static __constant__ PolyCoef kReluPolyTabD = poly_coef(false);
+static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
     ConstD d, dq;
 };
 __device__ __forceinline__ PolyTab poly_table() {
-    ConstD p = (ConstD)kReluPolyTabD;
-    ConstD q = (ConstD)kReluPolyTabDq;
+    ConstD p = (ConstD)kReluPolyTabD.c;
+    ConstD q = (ConstD)kReluPolyTabDq.c;
     asm volatile("" : "+s"(p), "+s"(q));
     return PolyTab{p, q};
 }

@@ -186,11 +186,18 @@ __device__ __forceinline__ void win_sums(const T (&w)[(R - 1) * S + TAPS], T (&o
 // inside the op instead of being hoisted out of the pair loop, where it would hold
 // registers for every geometry at once
 // (thread index within its 128-thread half: a two-pair workgroup runs one pair per half)
+#ifndef CGP_NET_OPAQUE_TID
+#define CGP_NET_OPAQUE_TID 1
+#endif
 __device__ __forceinline__ int opaque_tid() {
     static_assert(kNT == 128, "opaque_tid masks to 128-thread halves");
+#if CGP_NET_OPAQUE_TID
     int t;
     asm volatile("v_and_b32 %0, 0x7f, %1" : "=v"(t) : "v"((int)threadIdx.x));
     return t;
+#else
+    return (int)(threadIdx.x & 127u);
+#endif
 }
 
 // a / d for a >= 0 as an unsigned division (a constant d costs a mul-hi and a shift; the

@@ -19,8 +19,13 @@ HDR = os.path.join(PKG, "csrc", "relu_poly.h")
 
 
 def coeffs(kind):
+    """The coefficient table the default build compiles (the double one is selected by
+    CGP_RELU_DEG_D among several degrees)."""
     txt = open(HDR).read()
-    body = re.search(r"kReluPoly%s\[\d+\] = \{(.*?)\};" % kind, txt, re.S).group(1)
+    n = r"\d+"
+    if kind == "D":
+        n = str(int(re.search(r"#define CGP_RELU_DEG_D (\d+)", txt).group(1)) + 1)
+    body = re.search(r"kReluPoly%s\[%s\] = \{(.*?)\};" % (kind, n), txt, re.S).group(1)
     return [float(v.strip().rstrip("f")) for v in body.split(",") if v.strip()]
 
 
