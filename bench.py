@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--no-probe", action="store_true")
     p.add_argument("--no-second", action="store_true", help="skip the mnist_as_tf leg")
     p.add_argument("--no-fullscale", action="store_true")
+    p.add_argument("--no-fullscale-f32", action="store_true",
+                   help="skip the float32-kernel repeat of the full-scale leg")
     p.add_argument("--fullscale-n", type=int, default=60000)
     p.add_argument("--fullscale-m", type=int, default=10000)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -472,6 +474,21 @@ def main():
                           "re-evaluated through model(x_i, x_j)")
             extra["fullscale"] = fs
         torch.cuda.empty_cache()
+        if not args.no_fullscale_f32:
+            # the same pipeline at the reference pipeline's own kernel precision
+            # (save_kernel.py runs the float32 model; K stored float32, widened to float64
+            # for the solve by classify_gp.py's load_kern)
+            t0 = time.perf_counter()
+            fs = fullscale("mnist_as_tf", args.fullscale_n, args.fullscale_m, 4096,
+                           rank=rank, world=world, dev=dev, kernel_dtype=torch.float32)
+            if rank == 0:
+                fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
+                fs["note"] = ("kernels in float32 as exp_mnist_resnet/save_kernel.py runs "
+                              "them; K widened to float64 on the device for the rocSOLVER "
+                              "solve; spot_vs_f64_max_rel_err = float32 entries against "
+                              "the float64 model (north-star tolerance 1e-5)")
+                extra["fullscale_f32"] = fs
+            torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

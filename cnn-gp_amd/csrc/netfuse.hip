@@ -40,8 +40,14 @@ constexpr int kNT = CGP_NET_NT;  // threads per workgroup (one pair): two waves
 // (units u and u + 1, the same image i: the i-side variance loads of the halves meet in
 // L1 and each barrier serves both pairs; net_kernel); the small-map stages pack 4 / 16
 // pairs on two waves.  Ops only ever run on one half (NP = 1) or on NP = 4 / 16.
+#ifndef CGP_NET_SPLIT
+#define CGP_NET_SPLIT 2   // one-pair slices of a "2-pair" workgroup (A/B builds: 4)
+#endif
 template <int NP>
-constexpr int kNTof = NP == 2 ? 2 * kNT : kNT;
+constexpr int kNTof = NP == 2 ? CGP_NET_SPLIT * kNT : kNT;
+// pair units a workgroup takes per step of the walk
+template <int NP>
+constexpr int kUnitsOf = NP == 2 ? CGP_NET_SPLIT : NP;
 #ifndef CGP_NET_STL
 #define CGP_NET_STL 3
 #endif
@@ -1065,14 +1071,15 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     __shared__ unsigned pair_tab[2 * kMaxNP];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
-    for (int e = tid; e < NP * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
+    constexpr int UN = kUnitsOf<NP>;
+    for (int e = tid; e < UN * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
     lds_barrier();
     // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
     // contiguous run of supertiles and its L2 holds the images/variances they share.
     // Ranges and groups are whole multiples of NP units.
     const unsigned g8 = gridDim.x / 8, xcd = blockIdx.x % 8, l = blockIdx.x / 8;
     const long long span = p.uend - p.ubeg;
-    const long long per = ((span + 7) / 8 + NP - 1) / NP * NP;
+    const long long per = ((span + 7) / 8 + UN - 1) / UN * UN;
     const long long beg = p.ubeg + (long long)xcd * per;
     const long long end = beg + per < p.uend ? beg + per : p.uend;
 #if CGP_NET_DYN
@@ -1090,7 +1097,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     unsigned long long grab = 0;   // thread 0: the counter value fetched one pair ahead
     if (tid == 0) grab = atomicAdd(ctr, 1ull);
     auto advance = [&]() {
-        if (tid == 0) next_u[adv] = beg + (long long)grab * NP;
+        if (tid == 0) next_u[adv] = beg + (long long)grab * UN;
         lds_barrier();
         const long long v = next_u[adv];
         adv ^= 1;
@@ -1099,37 +1106,45 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     for (long long u = advance(); u < end; u = advance()) {
         if (tid == 0) grab = atomicAdd(ctr, 1ull);
 #else
-    for (long long u = beg + (long long)l * NP; u < end; u += (long long)g8 * NP) {
+    for (long long u = beg + (long long)l * UN; u < end; u += (long long)g8 * UN) {
 #endif
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
         if constexpr (NP == 2) {
-            // two one-pair halves sharing the workgroup's barriers: waves 0-1 run unit u,
-            // waves 2-3 unit u + 1 (the next j of the same image i), each on its own
-            // arena.  Every wave decodes both units (scalar), so the pair is uniform per
-            // wave and each half runs the one-pair code (scalar variance-map bases)
-            unsigned i0, j0, i1 = 0, j1 = 0;
-            const bool v0 = unit_pair(p, u, i0, j0);
-            const bool v1 = u + 1 < end && unit_pair(p, u + 1, i1, j1);
-            const bool w0 = v0 && !(p.same && j0 <= i0), w1 = v1 && !(p.same && j1 <= i1);
-            if (!w0 && !w1) {   // both below the diagonal of a same tile (or outside)
-                if (p.final_stage && p.same && tid == 0) {
-                    if (v0 && j0 == i0) p.out[(long long)i0 * p.ldo + i0] = p.kdiag[i0];
-                    if (v1 && j1 == i1) p.out[(long long)i1 * p.ldo + i1] = p.kdiag[i1];
+            // one-pair slices sharing the workgroup's barriers: waves 2q, 2q + 1 run unit
+            // u + q (the next j of the same image i), each on its own arena.  The pair is
+            // uniform per wave, so each slice runs the one-pair code (scalar variance-map
+            // bases)
+            // every wave decodes the group's units (scalar); the group is skipped only when
+            // none of them is evaluated, so all waves agree at every barrier
+            const int q = __builtin_amdgcn_readfirstlane(tid >> 7);
+            unsigned iq = 0, jq = 0;
+            bool vq = false, wq = false, any = false;
+#pragma unroll
+            for (int s = 0; s < UN; ++s) {
+                unsigned is = 0, js = 0;
+                const bool vs = u + s < end && unit_pair(p, u + s, is, js);
+                const bool ws = vs && !(p.same && js <= is);
+                any |= ws;
+                if (s == q) {
+                    iq = is;
+                    jq = js;
+                    vq = vs;
+                    wq = ws;
                 }
+            }
+            if (!any) {   // below the diagonal of a same tile (or outside): K[i, i] only
+                if (p.final_stage && p.same && (tid & (kNT - 1)) == 0 && vq && jq == iq)
+                    p.out[(long long)iq * p.ldo + iq] = p.kdiag[iq];
                 continue;
             }
-            const int q = __builtin_amdgcn_readfirstlane(tid >> 7);
-            const bool vq = q ? v1 : v0, wq = q ? w1 : w0;
             Pairs ph;
             ph.tab = pair_tab;
             ph.u0 = u + q;
-            // a half without a pair computes on clamped indices and stores nothing
-            ph.i = vq ? (q ? i1 : i0) : 0u;
-            ph.j = vq ? (q ? j1 : j0) : 0u;
-            ph.i = __builtin_amdgcn_readfirstlane(ph.i);
-            ph.j = __builtin_amdgcn_readfirstlane(ph.j);
+            // a slice without a pair computes on clamped indices and stores nothing
+            ph.i = __builtin_amdgcn_readfirstlane(vq ? iq : 0u);
+            ph.j = __builtin_amdgcn_readfirstlane(vq ? jq : 0u);
             T* lh = lds + q * p.lds_elems;
             const int ht = tid & (kNT - 1);
             if constexpr (PID < 0) {
@@ -1269,9 +1284,10 @@ const void* prog_fn_one() {
     if constexpr ((I.sizes & (int)sizeof(T)) == 0) {
         return nullptr;
     } else {
-        constexpr long long bytes = (long long)I.lds_elems * (long long)sizeof(T) * I.pairs;
+        constexpr long long bytes =
+            (long long)I.lds_elems * (long long)sizeof(T) * kUnitsOf<I.pairs>;
         constexpr int wpe = sizeof(T) == 8
-                                ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX, (I.pairs == 2 ? 2 * kNT : kNT) / 64)
+                                ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX, kNTof<I.pairs> / 64)
                                 : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
@@ -1289,6 +1305,8 @@ const void* prog_fn(int pid) {
 
 // threads of a workgroup of np pairs (kNTof at run time)
 int net_threads(int np) { return np == 2 ? kNTof<2> : kNT; }
+// pair units (arenas) a workgroup of np pairs holds
+int net_units(int np) { return np == 2 ? kUnitsOf<2> : np; }
 
 int net_occupancy(const void* fn, int lds_bytes, int threads) {
     if (lds_bytes > 64 * 1024 &&
@@ -1308,8 +1326,8 @@ int net_occupancy(const void* fn, int lds_bytes, int threads) {
 template <typename T>
 int net_occupancy_for(int lds_bytes, int flags, int np) {
     const void* fn = net_fn<T>(flags & CGP_FLAG_EXACT_RELU, flags & CGP_FLAG_NET_DUAL, np,
-                               (long long)lds_bytes * np);
-    return fn ? net_occupancy(fn, lds_bytes * np, net_threads(np)) : 0;
+                               (long long)lds_bytes * net_units(np));
+    return fn ? net_occupancy(fn, lds_bytes * net_units(np), net_threads(np)) : 0;
 }
 
 // Per-XCD unit counters for a launch: 8 × u64 slots of a 64-slot ring owned by the launch
@@ -1362,13 +1380,13 @@ unsigned long long* work_counters(hipStream_t s) {
 template <typename T>
 int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, int program,
                void* stream) {
-    const long long wg_bytes = lds_bytes * np;
+    const long long wg_bytes = lds_bytes * net_units(np);
     const void* fn = program > 0 && !ex ? prog_fn<T>(program - 1) : net_fn<T>(ex, du, np, wg_bytes);
     if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
     const int per_cu = net_occupancy(fn, (int)wg_bytes, net_threads(np));
     if (per_cu <= 0)
         return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", wg_bytes);
-    const long long groups = (p.uend - p.ubeg + np - 1) / np;
+    const long long groups = (p.uend - p.ubeg + net_units(np) - 1) / net_units(np);
     long long grid = (long long)per_cu * device_cus();
     if (grid > groups) grid = groups;
     grid = (grid + 7) / 8 * 8;                  // whole XCD rounds
@@ -1428,8 +1446,8 @@ int net_impl(const cgp_net_args* a, void* stream) {
     const int np = a->pairs <= 0 ? 1 : a->pairs;
     if (np != 1 && np != 2 && np != 4 && np != kMaxNP)
         return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 2, 4 or 16)", np);
-    if (lds_bytes * np > 160 * 1024)
-        return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * np);
+    if (lds_bytes * net_units(np) > 160 * 1024)
+        return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * net_units(np));
     // multi-pair stages address a pair's variance maps (<= 8 * threads / np pixels) with
     // 32-bit byte offsets (VarSrc)
     if (np > 1 && (a->n1 > a->n2 ? a->n1 : a->n2) * (8LL * net_threads(np) / np) *

@@ -50,7 +50,7 @@ def log(rank, msg):
         print(msg, flush=True)
 
 
-def build(model, X, X2, B, rank, world, name, t_start, dev, out=None):
+def build(model, X, X2, B, rank, world, name, t_start, dev, out=None, dtype=torch.float64):
     """This rank's tiles of Kxx (X2 None) or Kxz.  One rank: written straight into the
     NaN-filled device matrix ``out``.  Several ranks: packed into one flat device buffer
     (gram.gram_local's layout, split by evaluated pairs) for gather_gram.  Returns
@@ -62,7 +62,7 @@ def build(model, X, X2, B, rank, world, name, t_start, dev, out=None):
     if world > 1:
         cap = max(sum(a * b for *_, a, b in tile_plan(n, n2, B, r, world, split))
                   for r in range(world))
-        out = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
+        out = torch.empty(max(cap, 1), dtype=dtype, device=dev)
     pairs = 0
     off = 0
     last = time.perf_counter()
@@ -89,36 +89,52 @@ def build(model, X, X2, B, rank, world, name, t_start, dev, out=None):
     return out, pairs
 
 
+def widen(t):
+    """float32 device matrix -> float64 (classify_gp.py:45-48's load_kern widening, on the
+    device through cgp_cast_f32_f64); the float32 source is released."""
+    out = torch.empty(t.shape, dtype=torch.float64, device=t.device)
+    from cnn_gp import _native as N
+    N.call("cgp_cast_f32_f64", N.ptr(t), N.ptr(out), t.numel(),
+           torch.cuda.current_stream(t.device).cuda_stream)
+    return out
+
+
 def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spot=16,
-              pred_var=False, rank=0, world=1, dev=None, group=None):
+              pred_var=False, rank=0, world=1, dev=None, group=None,
+              kernel_dtype=torch.float64):
     """Kxx (n) + Kxz (m × n) + rocSOLVER solve + predict on the device; with world > 1
     the tiles are split over the ranks and gathered once to rank 0 (one RCCL gather per
-    matrix), which solves.  Returns the result dict on rank 0, None elsewhere."""
+    matrix), which solves.  Returns the result dict on rank 0, None elsewhere.
+
+    kernel_dtype float32 runs the kernels the way the reference's own pipeline does
+    (save_kernel.py:19-24: the float32 model on float32 images, K stored float32 by
+    kernel_save_tools.py:21) and widens K to float64 for the solve (classify_gp.py:45-48);
+    the spot check then also reports the float32 entries against the float64 model."""
     dev = dev or torch.device("cuda", torch.cuda.current_device())
     cfg = importlib.import_module(f"configs.{config}")
-    model = cfg.initial_model.to(dev, torch.float64)
+    model = cfg.initial_model.to(dev, kernel_dtype)
     C = getattr(cfg, "in_channels", 1)
     side = 32 if C == 3 else 28
-    X = mnist_like(n, C, side, 0).to(dev)
-    Z = mnist_like(m, C, side, 1).to(dev)
+    X = mnist_like(n, C, side, 0).to(dev, kernel_dtype)
+    Z = mnist_like(m, C, side, 1).to(dev, kernel_dtype)
     g = torch.Generator().manual_seed(2)
     ytr = torch.randint(0, 10, (n,), generator=g)
     yte = torch.randint(0, 10, (m,), generator=g)
     B = tile
-    res = {"config": config, "n": n, "m": m, "tile": B, "gpus": world}
+    res = {"config": config, "n": n, "m": m, "tile": B, "gpus": world,
+           "kernel_dtype": str(kernel_dtype).replace("torch.", "")}
+    kd = kernel_dtype
 
     if world > 1:
         dist.barrier(group)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    K = None if world > 1 else torch.full((n, n), float("nan"), dtype=torch.float64,
-                                          device=dev)
-    K, p_xx = build(model, X, None, B, rank, world, "Kxx", t0, dev, K)
+    K = None if world > 1 else torch.full((n, n), float("nan"), dtype=kd, device=dev)
+    K, p_xx = build(model, X, None, B, rank, world, "Kxx", t0, dev, K, kd)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    Kxz = None if world > 1 else torch.full((m, n), float("nan"), dtype=torch.float64,
-                                            device=dev)
-    Kxz, p_xz = build(model, Z, X, B, rank, world, "Kxz", t0, dev, Kxz)
+    Kxz = None if world > 1 else torch.full((m, n), float("nan"), dtype=kd, device=dev)
+    Kxz, p_xz = build(model, Z, X, B, rank, world, "Kxz", t0, dev, Kxz, kd)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     if world > 1:
@@ -152,6 +168,26 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
             ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
             worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
     res["spot_check_max_rel_err"] = worst
+    if kd != torch.float64:
+        # the float32 entries against the float64 model on the same (exactly widened)
+        # images: the north star's 1e-5 relative tolerance
+        m64 = cfg.initial_model.to(dev, torch.float64)
+        dev64 = 0.0
+        with torch.no_grad():
+            for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
+                a, b = min(a, b), max(a, b)
+                xa, xb = X[a:a + 1].double(), X[b:b + 1].double()
+                ref = m64(xa, xb, False, False).item() if a != b else m64(xa).item()
+                dev64 = max(dev64, abs(K[a, b].item() - ref) / abs(ref))
+                ref = m64(Z[c:c + 1].double(), xb, False, False).item()
+                dev64 = max(dev64, abs(Kxz[c, b].item() - ref) / abs(ref))
+        res["spot_vs_f64_max_rel_err"] = dev64
+        torch.cuda.synchronize()
+        tw = time.perf_counter()
+        K = widen(K)                    # the solve runs in float64 (classify_gp.py:19-22)
+        Kxz = widen(Kxz)
+        torch.cuda.synchronize()
+        res["widen_s"] = round(time.perf_counter() - tw, 3)
     # residual rows: K is symmetric, its upper triangle is filled
     rows = torch.randint(0, n, (8,), generator=gs).to(dev)
     Krows = torch.where(torch.arange(n, device=dev)[None, :] >= rows[:, None],
@@ -176,7 +212,7 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     if pred_var:
         with torch.no_grad():
             t7 = time.perf_counter()
-            kz = model(Z, Z, True, True)             # Kt_diag, save_kernel.py:33-36
+            kz = model(Z, Z, True, True).double()    # Kt_diag, save_kernel.py:33-36
             torch.cuda.synchronize()
             t8 = time.perf_counter()
             var = cnn_gp.predictive_variance(K, Kxz, kz, overwrite_kxz=True)
@@ -200,6 +236,9 @@ def main():
     ap.add_argument("--tile", type=int, default=4096)
     ap.add_argument("--jitter", type=float, default=0.0)
     ap.add_argument("--spot", type=int, default=16)
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"],
+                    help="kernel precision (f32: the reference pipeline's; K widened to "
+                         "f64 for the solve)")
     ap.add_argument("--pred-var", action="store_true",
                     help="also the posterior variance of the test points (prior diag "
                          "+ dtrsm on the factor), reported outside total_s")
@@ -212,7 +251,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     res = fullscale(args.config, args.n, args.m, args.tile, args.jitter, args.spot,
-                    args.pred_var, rank, world, dev)
+                    args.pred_var, rank, world, dev,
+                    kernel_dtype=torch.float64 if args.dtype == "f64" else torch.float32)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
