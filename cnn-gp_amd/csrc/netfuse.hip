@@ -1228,6 +1228,9 @@ constexpr int net_wpe(long long lds_bytes, int cap = 5, int waves = kNT / 64) {
     const long long w = wg * waves / 4;
     return w < 3 ? 3 : (w > cap ? cap : (int)w);
 }
+#ifndef CGP_NET_PROG_WPE_F32
+#define CGP_NET_PROG_WPE_F32 0   // > 0: fp32 programs' register target from their LDS, capped
+#endif
 #ifndef CGP_NET_PROG_WPE_MAX
 #define CGP_NET_PROG_WPE_MAX 5
 #endif
@@ -1288,7 +1291,9 @@ const void* prog_fn_one() {
             (long long)I.lds_elems * (long long)sizeof(T) * kUnitsOf<I.pairs>;
         constexpr int wpe = sizeof(T) == 8
                                 ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX, kNTof<I.pairs> / 64)
-                                : (I.dual ? 4 : 5);
+                                : CGP_NET_PROG_WPE_F32 > 0
+                                      ? net_wpe(bytes, CGP_NET_PROG_WPE_F32, kNTof<I.pairs> / 64)
+                                      : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
 }

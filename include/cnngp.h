@@ -277,8 +277,10 @@ typedef struct cgp_net_args {
     int32_t hs;            /* LDS offset of the row-sum scratch */
     int32_t lds_elems;     /* LDS footprint of ONE pair (elements of the compute type) */
     int32_t flags;         /* CGP_FLAG_EXACT_RELU */
-    int32_t pairs;         /* pairs per workgroup: 1, or 4 / 16 for a stage whose maps are
-                              at most 16x16 / 8x8 (each pair gets its own lds_elems arena) */
+    int32_t pairs;         /* pairs per workgroup: 1; 2 = two one-pair slices of a 256-thread
+                              workgroup (units u, u + 1: the same image i), any op list; or
+                              4 / 16 for a stage whose maps are at most 16x16 / 8x8 (each
+                              pair gets its own lds_elems arena) */
     int64_t unit_begin;    /* the tile's pair units this launch covers, [begin, end): unit */
     int64_t unit_end;      /* u = 64·supertile + 8·(i % 8) + j % 8; 0, 0 = the whole tile */
     int32_t final_stage;   /* 1: write K (the last stage); 0: the ops end in CGP_NET_STORE */
