@@ -302,11 +302,50 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = __builtin_fma(sx[r], p[r], c[r] + __builtin_fabs(c[r]));
 }
+// fp32: pixels in pairs on the packed-fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32 do two fp32 lanes per instruction at the rate of one).  Each element sees
+// exactly relu_fast's IEEE operations in the same order, so the packed form is
+// bit-identical to the scalar one; only min/max/abs and the rsq estimates stay scalar (no
+// packed form).  An odd R leaves one pixel on the scalar path.
+#ifndef CGP_F32_PACKED
+#define CGP_F32_PACKED 1
+#endif
+typedef float cgp_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cgp_f2 relu_fast2(cgp_f2 c, cgp_f2 v1, cgp_f2 v2) {
+    const cgp_f2 t = __builtin_elementwise_fma(v1, v2, cgp_f2(K<float>::tiny));
+    const cgp_f2 y = {__builtin_amdgcn_rsqf(t.x), __builtin_amdgcn_rsqf(t.y)};
+    const cgp_f2 st = t * y;                                   // sqrt(t)
+    const cgp_f2 cy = c * y;
+    const cgp_f2 a = {__builtin_fminf(__builtin_fabsf(cy.x), 1.0f),
+                      __builtin_fminf(__builtin_fabsf(cy.y), 1.0f)};   // |rho| clamped
+    const cgp_f2 x = __builtin_elementwise_fma(cgp_f2(-0.5f), a, cgp_f2(0.5f));
+    const cgp_f2 xm = {__builtin_fmaxf(x.x, K<float>::xfloor), __builtin_fmaxf(x.y, K<float>::xfloor)};
+    const cgp_f2 h = {__builtin_amdgcn_rsqf(xm.x), __builtin_amdgcn_rsqf(xm.y)};
+    const cgp_f2 sx = xm * h;                                  // sqrt(x)
+    cgp_f2 p = cgp_f2(kReluPolyF[kReluPolyDegF]);
+#pragma unroll
+    for (int k = kReluPolyDegF - 1; k >= 0; --k)
+        p = __builtin_elementwise_fma(p, x, cgp_f2(kReluPolyF[k]));
+    const cgp_f2 ac = {__builtin_fabsf(c.x), __builtin_fabsf(c.y)};
+    const cgp_f2 hpos = (c + ac) * cgp_f2(0.25f);              // max(c, 0) / 2
+    return __builtin_elementwise_fma((st * x) * sx, p, hpos);
+}
 template <int R>
 __device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],
                                             const float (&v2)[R], const PolyTab& tab) {
+#if CGP_F32_PACKED
+#pragma unroll
+    for (int r = 0; r + 1 < R; r += 2) {
+        const cgp_f2 o = relu_fast2(cgp_f2{c[r], c[r + 1]}, cgp_f2{v1[r], v1[r + 1]},
+                                    cgp_f2{v2[r], v2[r + 1]});
+        c[r] = o.x;
+        c[r + 1] = o.y;
+    }
+    if constexpr (R % 2) c[R - 1] = relu_fast(c[R - 1], v1[R - 1], v2[R - 1], tab);
+#else
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = relu_fast(c[r], v1[r], v2[r], tab);
+#endif
 }
 
 template <typename T>
