@@ -75,6 +75,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-probe", action="store_true")
     p.add_argument("--no-second", action="store_true", help="skip the mnist_as_tf leg")
+    p.add_argument("--no-f32", action="store_true",
+                   help="skip the float32 repeat of the Kxx legs")
     p.add_argument("--no-fullscale", action="store_true")
     p.add_argument("--no-fullscale-f32", action="store_true",
                    help="skip the float32-kernel repeat of the full-scale leg")
@@ -458,6 +460,27 @@ def main():
                 "roofline": net_roofline(r2["model"], r2["X"][:B], "mnist_as_tf",
                                          r2["timing"]) if probe else None}
         torch.cuda.empty_cache()
+
+    # --- the same two workloads at the reference pipeline's own kernel precision ---
+    # (exp_mnist_resnet/save_kernel.py runs the float32 model; kernel_save_tools.py:21
+    # stores K as float32).  Reported beside the fp64 headline, never as `value`.
+    if not args.no_f32 and dtype == torch.float64:
+        f32 = {}
+        for name in ((args.config,) if args.no_second or args.config == "mnist_as_tf"
+                     else (args.config, "mnist_as_tf")):
+            r3 = time_config(name, args.n, B, max(2, args.steps // 2), 1, world, rank, dev,
+                             torch.float32, backend, False)
+            del r3["K"]
+            f32[name] = {"value": round(r3["value"], 1), "unit": "pairs/s",
+                         "ms_per_step": round(r3["ms_step"], 3),
+                         "pairs_per_step": r3["evaluated"]}
+            torch.cuda.empty_cache()
+        if rank == 0:
+            f32["note"] = ("float32 model and images, as the reference's save_kernel.py runs "
+                           "them; same Kxx harness as the fp64 legs.  Entries stay within "
+                           "3e-7 relative of the fp64 kernel (tests/test_gpu_parity.py "
+                           "test_f32_kernel_within_north_star_tolerance; north star 1e-5)")
+            extra["f32"] = f32
 
     # --- BASELINE configs[3]: the full-scale ResNet-GP pipeline ---
     if not args.no_fullscale and dtype == torch.float64:
