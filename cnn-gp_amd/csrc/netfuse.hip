@@ -713,8 +713,14 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
                    : var_src<T, NP == 1>(op, iq, jq, hw);
     };
     const VarSrc<T> vs0 = vs_of(pr.i, pr.j);
-    const GP<T> xi = gptr<T>(p.x) + (size_t)pr.i * p.channels * hw;
-    const GP<T> yj = gptr<T>(p.y) + (size_t)pr.j * p.channels * hw;
+    // the pair's images (MOMENTS, one pair per half: i, j uniform) as scalar byte bases;
+    // pixel offsets stay 32-bit unsigned, so every load is SGPR base + VGPR offset with no
+    // 64-bit VALU address arithmetic (an image is at most C·hw·8 bytes)
+    const GP<char> xi = ubase(p.x) + (size_t)pr.i * p.channels * hw * sizeof(T);
+    const GP<char> yj = ubase(p.y) + (size_t)pr.j * p.channels * hw * sizeof(T);
+    auto img = [](GP<char> b, unsigned e) {
+        return *(GP<T>)(b + (size_t)(e * (unsigned)sizeof(T)));
+    };
     const int n = NP * hw;
     // waves with no pixel in this pass skip the ReLUs (uniform per wave)
     const bool live = base + (tid & ~63) < n;
@@ -741,9 +747,11 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
             static_assert(NP == 1, "moments run one pair per workgroup (half)");
-            T acc = xi[pc] * yj[pc];
-            for (int ch = 1; ch < p.channels; ++ch)
-                acc += xi[(size_t)ch * hw + pc] * yj[(size_t)ch * hw + pc];
+            T acc = img(xi, (unsigned)pc) * img(yj, (unsigned)pc);
+            for (int ch = 1; ch < p.channels; ++ch) {
+                const unsigned e = (unsigned)(ch * hw + pc);
+                acc += img(xi, e) * img(yj, e);
+            }
             a[k] = acc;
         } else {
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
