@@ -579,8 +579,12 @@ class NetPlan:
                 var[v] = (q, vy)
         for sidx, st in enumerate(self.stages):
             arr = self._ops_array(st, var, states[sidx], states[sidx + 1])
-            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-            ops_dev = host.to(x.device)             # stream-ordered, freed stream-ordered
+            # pinned + non_blocking: a pageable H2D copy would block the host until the
+            # previous tile's kernels drained, leaving the GPU idle while this tile's small
+            # launches are issued; the caching host allocator keeps the pinned block until
+            # the copy has run
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).pin_memory()
+            ops_dev = host.to(x.device, non_blocking=True)   # stream-ordered, freed stream-ordered
             keep.append(ops_dev)
             a = N.NetArgs()
             a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
