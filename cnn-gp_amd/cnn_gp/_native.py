@@ -105,6 +105,7 @@ SIGNATURES = {
     "cgp_var_relu_f32": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
     "cgp_axpby_f64": (_i32, [_f64, _vp, _f64, _vp, _vp, _i64, _vp]),
     "cgp_axpby_f32": (_i32, [_f64, _vp, _f64, _vp, _vp, _i64, _vp]),
+    "cgp_scale_batch_f64": (_i32, [_i32, _vp, _vp, _vp, _f64, _vp]),
     "cgp_cast_f32_f64": (_i32, [_vp, _vp, _i64, _vp]),
     "cgp_transpose_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_chol_solve_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,

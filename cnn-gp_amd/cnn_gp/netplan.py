@@ -604,10 +604,15 @@ class NetPlan:
 
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2
 
+        if quarters:   # one launch fills every quartered map
+            nq = len(quarters)
+            q_src = (ctypes.c_void_p * nq)(*[N.ptr(s_) for s_, _ in quarters])
+            q_dst = (ctypes.c_void_p * nq)(*[N.ptr(q_) for _, q_ in quarters])
+            q_n = (ctypes.c_int64 * nq)(*[s_.numel() for s_, _ in quarters])
+
         def run_all(stream):
-            for src, q in quarters:
-                N.call("cgp_axpby_f64", 0.25, N.ptr(src), 0.0, None, N.ptr(q), src.numel(),
-                       stream)
+            if quarters:
+                N.call("cgp_scale_batch_f64", nq, q_src, q_dst, q_n, 0.25, stream)
             for u0 in range(0, units, chunk):
                 u1 = min(units, u0 + chunk)
                 for a in launches:

@@ -704,6 +704,25 @@ __global__ __launch_bounds__(kBlock) void axpby_kernel(T alpha, const T* __restr
     }
 }
 
+// dst_k = alpha·src_k for up to kScaleBatch buffers in one launch (blockIdx.y = buffer):
+// the fp64 whole-network kernel's quartered x-side variance maps, one launch per tile
+// instead of one per map
+constexpr int kScaleBatch = 32;
+struct ScaleBatch {
+    const double* src[kScaleBatch];
+    double* dst[kScaleBatch];
+    long long n[kScaleBatch];
+};
+__global__ __launch_bounds__(kBlock) void scale_batch_kernel(ScaleBatch b, double alpha) {
+    const int k = blockIdx.y;
+    const double* __restrict__ src = b.src[k];
+    double* __restrict__ dst = b.dst[k];
+    const long long n = b.n[k];
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride)
+        dst[e] = alpha * src[e];
+}
+
 __global__ __launch_bounds__(kBlock) void cast_kernel(const float* __restrict__ in,
                                                       double* __restrict__ out, long long n) {
     const long long stride = (long long)gridDim.x * kBlock;
@@ -1214,6 +1233,30 @@ int cgp_var_relu_f32(const float* xx, const float* yy, int64_t n1, int64_t n2, i
 int cgp_axpby_f64(double alpha, const double* a, double beta, const double* b, double* out,
                   int64_t n, void* stream) {
     return axpby_impl<double>(alpha, a, beta, b, out, n, stream);
+}
+int cgp_scale_batch_f64(int32_t count, const double* const* src, double* const* dst,
+                        const int64_t* n, double alpha, void* stream) {
+    if (count < 0 || (count > 0 && (!src || !dst || !n)))
+        return fail(CGP_EINVAL, "scale_batch: bad arguments");
+    for (int base = 0; base < count; base += kScaleBatch) {
+        ScaleBatch b{};
+        long long most = 0;
+        const int m = count - base < kScaleBatch ? count - base : kScaleBatch;
+        for (int k = 0; k < m; ++k) {
+            b.src[k] = src[base + k];
+            b.dst[k] = dst[base + k];
+            b.n[k] = n[base + k];
+            if (b.n[k] < 0 || (b.n[k] > 0 && (!b.src[k] || !b.dst[k])))
+                return fail(CGP_EINVAL, "scale_batch: buffer %d", base + k);
+            if (b.n[k] > most) most = b.n[k];
+        }
+        if (most == 0) continue;
+        hipLaunchKernelGGL(scale_batch_kernel, dim3(grid_for(most), m), dim3(kBlock), 0,
+                           as_stream(stream), b, alpha);
+        const int rc = check_launch("scale_batch_kernel");
+        if (rc != CGP_OK) return rc;
+    }
+    return CGP_OK;
 }
 int cgp_axpby_f32(double alpha, const float* a, double beta, const float* b, float* out,
                   int64_t n, void* stream) {

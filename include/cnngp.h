@@ -161,6 +161,15 @@ int cgp_axpby_f64(double alpha, const double* a, double beta, const double* b, d
 int cgp_axpby_f32(double alpha, const float* a, double beta, const float* b, float* out,
                   int64_t n, void* stream);
 
+/*
+ * dst[k] = alpha·src[k] (n[k] elements) for count buffers, in one launch per 32 (host
+ * arrays of device pointers).  No reference counterpart: it fills the quartered x-side
+ * variance maps the fp64 closed-form ReLU of cgp_net_f64 reads (one launch per tile instead
+ * of one cgp_axpby_f64 per map; cnn_gp/netplan.py).
+ */
+int cgp_scale_batch_f64(int32_t count, const double* const* src, double* const* dst,
+                        const int64_t* n, double alpha, void* stream);
+
 /* load_kern's float32 → float64 widening, classify_gp.py:45-48 */
 int cgp_cast_f32_f64(const float* in, double* out, int64_t n, void* stream);
 /* dst[c][r] = src[r][c]; src [rows][cols] row-major */

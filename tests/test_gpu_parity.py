@@ -695,3 +695,20 @@ def test_large_tile_properties(cfg, monkeypatch):
     sol = cnn_gp.solve_system(K.clone(), Y)
     r = (K @ sol - Y).norm() / Y.norm()
     assert float(r) < 1e-6
+
+
+def test_scale_batch_quarters_every_buffer():
+    """cgp_scale_batch_f64 (the quartered x-side variance maps of the fp64 net kernel):
+    bit-exact alpha·src for many buffers of unequal sizes, empty ones and more than one
+    launch's worth (32 per launch)"""
+    g = torch.Generator().manual_seed(5)
+    sizes = [784, 1, 0, 196 * 1024, 49, 5000] * 7          # 42 buffers: two launches
+    src = [torch.rand(n, generator=g, dtype=torch.float64).to(DEV) for n in sizes]
+    dst = [torch.full_like(s, float("nan")) for s in src]
+    k = len(src)
+    ps = (ctypes.c_void_p * k)(*[s.data_ptr() for s in src])
+    pd = (ctypes.c_void_p * k)(*[d.data_ptr() for d in dst])
+    pn = (ctypes.c_int64 * k)(*sizes)
+    N.call("cgp_scale_batch_f64", k, ps, pd, pn, 0.25, stream())
+    for s, d in zip(src, dst):
+        assert torch.equal(d, s * 0.25)

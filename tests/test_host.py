@@ -77,6 +77,8 @@ def test_invalid_arguments_rejected_on_host():
     r = N.ReluArgs()
     assert lib.cgp_relu_f64(ctypes.byref(r), None) == 1001
     assert lib.cgp_axpby_f64(1.0, None, 1.0, None, None, 10, None) == 1001
+    assert lib.cgp_scale_batch_f64(2, None, None, None, 0.25, None) == 1001
+    assert lib.cgp_scale_batch_f64(0, None, None, None, 0.25, None) == 0
 
 
 def test_forward_without_gpu_fails_loudly():
