@@ -117,7 +117,9 @@ def first_pairs(n_stages: int) -> int:
     del n_stages
     return 2 if FIRST_PAIRS in ("2", "auto") else 1
 MIN_STAGE_OPS = 4                      # a shorter tail is not worth a launch + state
-CHUNK_BYTES = 1 << 30                  # state buffers: units per launch group
+# state buffers: units per launch group (each group runs every stage once, and each launch
+# ends in a tail where the last workgroups finish their pairs)
+CHUNK_BYTES = int(os.environ.get("CGP_NET_CHUNK_MB", "8192")) << 20
 
 
 class NetPlan:
