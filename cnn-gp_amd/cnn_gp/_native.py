@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 6
+CGP_ABI_VERSION = 7
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -22,6 +22,7 @@ CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
 CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
 CGP_NET_LOAD, CGP_NET_STORE = 4, 5
+CGP_VAR_MOMENTS, CGP_VAR_CONV, CGP_VAR_HALF, CGP_VAR_SUM = 0, 1, 2, 3
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -61,6 +62,27 @@ class NetOp(ctypes.Structure):
         ("dst2", _i32), ("zero_halo", _i32),
         ("weight", _f64), ("bias", _f64), ("var_x", _vp), ("var_y", _vp),
         ("var2_x", _vp), ("var2_y", _vp),
+    ]
+
+
+class VarOp(ctypes.Structure):
+    """Mirror of cgp_var_op (include/cnngp.h)."""
+    _fields_ = [
+        ("kind", _i32), ("dst", _i32), ("src", _i32 * 4),
+        ("h", _i32), ("w", _i32), ("ho", _i32), ("wo", _i32),
+        ("taps", _i32), ("offset", _i32), ("stride", _i32), ("dilation", _i32),
+        ("store", _i64), ("qstore", _i64),
+        ("weight", _f64), ("bias", _f64), ("coef", _f64 * 4),
+    ]
+
+
+class VarArgs(ctypes.Structure):
+    """Mirror of cgp_var_args (include/cnngp.h)."""
+    _fields_ = [
+        ("x", _vp), ("y", _vp), ("out", _vp), ("ops", _vp),
+        ("n1", _i64), ("n2", _i64), ("store_total", _i64),
+        ("nops", _i32), ("channels", _i32), ("h", _i32), ("w", _i32),
+        ("lds_elems", _i32), ("scratch", _i32),
     ]
 
 
@@ -123,6 +145,10 @@ SIGNATURES = {
     "cgp_net_program": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32]),
     "cgp_net_f64": (_i32, [ctypes.POINTER(NetArgs), _vp]),
     "cgp_net_f32": (_i32, [ctypes.POINTER(NetArgs), _vp]),
+    "cgp_var_op_size": (ctypes.c_size_t, []),
+    "cgp_var_args_size": (ctypes.c_size_t, []),
+    "cgp_var_chain_f64": (_i32, [ctypes.POINTER(VarArgs), _vp]),
+    "cgp_var_chain_f32": (_i32, [ctypes.POINTER(VarArgs), _vp]),
 }
 
 _lib = None
@@ -158,7 +184,9 @@ def load():
         if lib.cgp_conv_args_size() != ctypes.sizeof(ConvArgs) or \
                 lib.cgp_relu_args_size() != ctypes.sizeof(ReluArgs) or \
                 lib.cgp_net_op_size() != ctypes.sizeof(NetOp) or \
-                lib.cgp_net_args_size() != ctypes.sizeof(NetArgs):
+                lib.cgp_net_args_size() != ctypes.sizeof(NetArgs) or \
+                lib.cgp_var_op_size() != ctypes.sizeof(VarOp) or \
+                lib.cgp_var_args_size() != ctypes.sizeof(VarArgs):
             _lib_err = "libcnngp.so argument struct layout differs from _native.py"
             raise RuntimeError(_lib_err)
         _lib = lib

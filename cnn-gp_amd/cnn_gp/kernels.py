@@ -7,12 +7,18 @@ storage only: no torch compute runs on the pair maps.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import _native as N
 from .program import Plan
+
+# the whole-network path computes the per-image variance maps with one cgp_var_chain launch
+# (CGP_VAR_CHAIN=0: the layer-by-layer variance pipeline, one launch per op)
+VAR_CHAIN = os.environ.get("CGP_VAR_CHAIN", "1") != "0"
 
 __all__ = ("NNGPKernel", "Conv2d", "ReLU", "Sequential", "Mixture", "Sum", "resnet_block")
 
@@ -128,12 +134,20 @@ class NNGPKernel(nn.Module):
         plan = self._plan(h, w)
         sfx = Plan._sfx(x.dtype)
         lib = N.load()
+        net = None if diag else self._net_plan(plan, x.element_size())
+        if net is not None and VAR_CHAIN:
+            # every variance map in one launch (cgp_var_chain_*), quartered x-side copies
+            # included (kernels.py:44-49 moments, then the program on each image)
+            fused = plan.run_variances_fused(x, y, n1, n2, same, stream, net.need_var,
+                                             net.quarter_vars(x.dtype, plan.flags))
+            if fused is not None:
+                var, qvar = fused
+                return net.run(x, y, var, n1, n2, same, stream, plan.flags, qvar=qvar)
         # per-image variances of the inputs (kernels.py:48-49)
         var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=x.device)
         N.check(getattr(lib, f"cgp_moments_var_{sfx}")(N.ptr(x), N.ptr(y), n1, n2, c, h * w,
                                                         N.ptr(var0[:n1]), N.ptr(var0[n1:]),
                                                         stream), "cgp_moments_var")
-        net = None if diag else self._net_plan(plan, x.element_size())
         if net is not None:                                      # whole-network kernel
             var = plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, stream,
                                      need=net.need_var)

@@ -539,8 +539,10 @@ class NetPlan:
         return (nbi * (nbi + 1) // 2 if same else nbi * nbj) * st * st
 
     def prepare(self, x, y, var, n1: int, n2: int, same: bool, flags: int = 0,
-                out: Optional[torch.Tensor] = None):
+                out: Optional[torch.Tensor] = None, qvar: Optional[dict] = None):
         """Upload the op lists for these variance maps; return (launch(stream), out).
+        ``qvar``: the quartered x-side maps (program.Plan.run_variances_fused), else they
+        are filled here with cgp_scale_batch_f64.
         ``out`` may be a row-strided view (e.g. a tile of a larger K): the kernel writes
         K[i, j] at out[i * out.stride(0) + j]."""
         sfx = "f64" if x.dtype == torch.float64 else "f32"
@@ -567,14 +569,14 @@ class NetPlan:
         # maps quartered (an exact scaling that folds its Newton steps' halvings); the
         # copies are filled on the launch stream before the kernels
         quarters = []
-        if x.dtype == torch.float64 and not flags & N.CGP_FLAG_EXACT_RELU and QUARTER_MAPS:
-            used = set()
-            for st in self.stages:
-                used |= {v for _, v in st.records if v is not None}
-                used |= {f["var2"] for f, _ in st.records if "var2" in f}
+        used = self.quarter_vars(x.dtype, flags)
+        if used:
             var = dict(var)
             for v in sorted(used):
                 vx, vy = var[v]
+                if qvar is not None:           # filled by the variance chain already
+                    var[v] = (qvar[v], vy)
+                    continue
                 q = torch.empty_like(vx)
                 quarters.append((vx, q))
                 keep.append(q)
@@ -646,10 +648,20 @@ class NetPlan:
 
         return launch, out
 
+    def quarter_vars(self, dtype, flags: int = 0) -> set:
+        """Values whose x-side variance maps the fp64 closed-form ReLU reads quartered."""
+        if dtype != torch.float64 or flags & N.CGP_FLAG_EXACT_RELU or not QUARTER_MAPS:
+            return set()
+        used = set()
+        for st in self.stages:
+            used |= {v for _, v in st.records if v is not None}
+            used |= {f["var2"] for f, _ in st.records if "var2" in f}
+        return used
+
     def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
-            out: Optional[torch.Tensor] = None):
+            out: Optional[torch.Tensor] = None, qvar: Optional[dict] = None):
         """K tile [n1, n2] of the pairs (x_i, y_j).  var: value -> (xx [n1,..], yy [n2,..])
         for every value in ``need_var``."""
-        launch, out = self.prepare(x, y, var, n1, n2, same, flags, out)
+        launch, out = self.prepare(x, y, var, n1, n2, same, flags, out, qvar)
         launch(stream)
         return out

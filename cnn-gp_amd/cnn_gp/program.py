@@ -373,6 +373,127 @@ class Plan:
                 del vals[v]
         return keep
 
+    # -- the same program in one launch (cgp_var_chain_*) --------------------------------
+    def _var_chain(self, need, quarter, dev):
+        """cgp_var_op records of the variance program (cached per need/quarter/device):
+        LDS slots by first fit over the values' live ranges, store offsets per image.
+        None when the program has an op the chain kernel lacks (a Sum of > 4 terms)."""
+        key = (frozenset(need), frozenset(quarter), str(dev))
+        cache = self.__dict__.setdefault("_var_chains", {})
+        if key in cache:
+            return cache[key]
+        ops = self.prog.ops
+        shapes = self.prog.shapes
+        last = self._last_use(ops, self.vf)
+        free = []                                  # (start, size) free LDS ranges
+        top = [0]
+        slot = {}
+
+        def alloc(v):
+            size = shapes[v][0] * shapes[v][1]
+            size += size & 1                       # 16-byte aligned fp64 slots
+            for k, (st, sz) in enumerate(free):
+                if sz >= size:
+                    free[k] = (st + size, sz - size)
+                    slot[v] = st
+                    return st
+            slot[v] = top[0]
+            top[0] += size
+            return slot[v]
+
+        def release(v):
+            size = shapes[v][0] * shapes[v][1]
+            free.append((slot.pop(v), size + (size & 1)))
+
+        store, qstore, total, qtotal = {}, {}, 0, 0
+
+        def stored(v):
+            nonlocal total, qtotal
+            if v not in need:
+                return -1, -1
+            hw = shapes[v][0] * shapes[v][1]
+            store[v], total = total, total + hw
+            if v in quarter:
+                qstore[v], qtotal = qtotal, qtotal + hw
+            return store[v], qstore.get(v, -1)
+
+        recs = []
+        h, w = shapes[self.v0]
+        r = N.VarOp(kind=N.CGP_VAR_MOMENTS, dst=alloc(self.v0), h=h, w=w, ho=h, wo=w)
+        r.src[:] = [-1, -1, -1, -1]
+        r.store, r.qstore = stored(self.v0)
+        recs.append(r)
+        for idx, op in enumerate(ops):
+            srcs = [op.src] if op.kind in ("conv", "relu") else [t for _, t in op.terms]
+            if len(srcs) > 4:
+                cache[key] = None
+                return None
+            r = N.VarOp(dst=alloc(op.dst))
+            r.src[:] = [slot[s] for s in srcs] + [-1] * (4 - len(srcs))
+            (r.h, r.w), (r.ho, r.wo) = shapes[srcs[0]], op.shape_out
+            if op.kind == "conv":
+                g = op.geom
+                r.kind = N.CGP_VAR_CONV
+                r.taps, r.offset, r.stride, r.dilation = g.taps, g.offset, g.stride, g.dilation
+                r.weight, r.bias = g.weight, g.bias
+            elif op.kind == "relu":
+                r.kind = N.CGP_VAR_HALF
+            else:
+                r.kind = N.CGP_VAR_SUM
+                r.coef[:] = [1.0 if c is None else float(c) for c, _ in op.terms] + \
+                    [0.0] * (4 - len(op.terms))
+            r.store, r.qstore = stored(op.dst)
+            recs.append(r)
+            for s in set(srcs):
+                if last.get(s, -1) <= idx and s in slot:
+                    release(s)
+            if last.get(op.dst, -1) <= idx and op.dst != self.vf:
+                release(op.dst)
+        # the convs' row-sum scratch after the slots: [h][wo] of the largest conv
+        scratch = top[0]
+        hs = max([r.h * r.wo for r in recs if r.kind == N.CGP_VAR_CONV] + [2])
+        top[0] += hs + (hs & 1)
+        arr = (N.VarOp * len(recs))(*recs)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).pin_memory()
+        chain = dict(ops=host.to(dev, non_blocking=True), nops=len(recs), lds=top[0],
+                     scratch=scratch,
+                     store=store, qstore=qstore, total=total, qtotal=qtotal)
+        cache[key] = chain
+        return chain
+
+    def run_variances_fused(self, x, y, n1, n2, same, stream, need, quarter=()):
+        """run_variances in one launch.  Returns (var, qvar): var[v] = (xx [n1,..],
+        yy [n2,..]) for v in need (yy is xx when same), qvar[v] = xx / 4 for v in quarter;
+        None when the chain kernel cannot run this program."""
+        need = set(need)
+        quarter = set(quarter) & need
+        chain = self._var_chain(need, quarter, x.device)
+        if chain is None or chain["lds"] * x.element_size() > 64 * 1024:
+            return None
+        m2 = 0 if same else n2
+        n = n1 + m2
+        out = torch.empty((n * chain["total"] + n1 * chain["qtotal"],), dtype=x.dtype,
+                          device=x.device)
+        a = N.VarArgs()
+        a.x, a.y, a.out, a.ops = x.data_ptr(), y.data_ptr(), out.data_ptr(), \
+            chain["ops"].data_ptr()
+        a.n1, a.n2, a.store_total = n1, m2, chain["total"]
+        a.nops, a.channels, a.h, a.w = chain["nops"], x.shape[1], x.shape[2], x.shape[3]
+        a.lds_elems, a.scratch = chain["lds"], chain["scratch"]
+        N.check(getattr(N.load(), f"cgp_var_chain_{self._sfx(x.dtype)}")(a, stream),
+                "cgp_var_chain")
+        shapes = self.prog.shapes
+        var, qvar = {}, {}
+        for v, off in chain["store"].items():
+            ho, wo = shapes[v]
+            blk = out[n * off:n * (off + ho * wo)].view(n, ho, wo)
+            var[v] = (blk[:n1], blk[:n1] if same else blk[n1:])
+        for v, off in chain["qstore"].items():
+            ho, wo = shapes[v]
+            base = n * chain["total"] + n1 * off
+            qvar[v] = out[base:base + n1 * ho * wo].view(n1, ho, wo)
+        return var, qvar
+
     # -- pair pipeline ------------------------------------------------------------------
     def run_pairs(self, x, y, xy0, var, n1, n2, same, diag, stream, probe=None):
         """Runs the fused pair program; returns the final [nmaps, fh, fw] tensor.

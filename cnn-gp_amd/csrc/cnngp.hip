@@ -770,6 +770,123 @@ __global__ __launch_bounds__(kBlock) void row_sumsq_sub_kernel(const double* __r
     }
 }
 
+// ---- the variance chain (cgp_var_chain_*): every per-image variance map of a network in
+// one launch.  A workgroup walks image g through the op list in LDS (slots from the host);
+// the stored maps go to out (layout in cnngp.h).  Same rounding as the layer kernels it
+// replaces: moments acc = x0·x0 + x1·x1 + ... then / C; conv w·Σ + b as two roundings;
+// Sums as the axpby chain (c0·t0, then o + c_k·t_k).
+template <typename T>
+struct VarChainP {
+    const T* x;
+    const T* y;
+    T* out;
+    const cgp_var_op* ops;
+    long long n1, n2, store_total;
+    int nops, channels, hw_in, lds_elems, scratch;
+};
+template <typename T>
+__global__ __launch_bounds__(kBlock) void var_chain_kernel(const VarChainP<T> p) {
+    extern __shared__ __align__(16) unsigned char var_smem[];
+    T* lds = reinterpret_cast<T*>(var_smem);
+    const long long n = p.n1 + p.n2;
+    for (long long g = blockIdx.x; g < n; g += gridDim.x) {
+        const T* img = g < p.n1 ? p.x + g * p.channels * p.hw_in
+                                : p.y + (g - p.n1) * p.channels * p.hw_in;
+        for (int k = 0; k < p.nops; ++k) {
+            const cgp_var_op op = p.ops[k];
+            const int howo = op.ho * op.wo;
+            T* dst = lds + op.dst;
+            if (op.kind == CGP_VAR_MOMENTS) {
+                for (int e = threadIdx.x; e < howo; e += kBlock) {
+                    T acc = img[e] * img[e];
+                    for (int c = 1; c < p.channels; ++c) {
+                        const T v = img[(size_t)c * p.hw_in + e];
+                        acc += v * v;
+                    }
+                    dst[e] = acc / T(p.channels);
+                }
+            } else if (op.kind == CGP_VAR_CONV) {
+                // separable like the layer kernels: window sums along each input row into
+                // the scratch, then along columns (a full-window conv stays parallel)
+                const T* src = lds + op.src[0];
+                T* hs = lds + p.scratch;
+                const T w = (T)op.weight, b = (T)op.bias;
+                for (int e = threadIdx.x; e < op.h * op.wo; e += kBlock) {
+                    const int r = e / op.wo, co = e - r * op.wo;
+                    T acc = T(0);
+                    for (int dx = 0; dx < op.taps; ++dx) {
+                        const int c = co * op.stride + op.offset + dx * op.dilation;
+                        if (c >= 0 && c < op.w) acc += src[r * op.w + c];
+                    }
+                    hs[e] = acc;
+                }
+                __syncthreads();
+                for (int e = threadIdx.x; e < howo; e += kBlock) {
+                    const int ro = e / op.wo, co = e - ro * op.wo;
+                    T acc = T(0);
+                    for (int dy = 0; dy < op.taps; ++dy) {
+                        const int r = ro * op.stride + op.offset + dy * op.dilation;
+                        if (r >= 0 && r < op.h) acc += hs[r * op.wo + co];
+                    }
+                    dst[e] = w * acc + b;
+                }
+            } else if (op.kind == CGP_VAR_HALF) {
+                const T* src = lds + op.src[0];
+                for (int e = threadIdx.x; e < howo; e += kBlock) dst[e] = src[e] / T(2);
+            } else {   // CGP_VAR_SUM
+                for (int e = threadIdx.x; e < howo; e += kBlock) {
+                    T acc = (T)op.coef[0] * lds[op.src[0] + e];
+                    for (int t = 1; t < 4 && op.src[t] >= 0; ++t)
+                        acc = acc + (T)op.coef[t] * lds[op.src[t] + e];
+                    dst[e] = acc;
+                }
+            }
+            __syncthreads();
+            if (op.store >= 0) {
+                T* o = p.out + n * op.store + g * howo;
+                for (int e = threadIdx.x; e < howo; e += kBlock) o[e] = dst[e];
+                if (op.qstore >= 0 && g < p.n1) {
+                    T* q = p.out + n * p.store_total + p.n1 * op.qstore + g * howo;
+                    for (int e = threadIdx.x; e < howo; e += kBlock) q[e] = T(0.25) * dst[e];
+                }
+                __syncthreads();   // a later op may reuse the slot
+            }
+        }
+    }
+}
+
+template <typename T>
+int var_chain_impl(const cgp_var_args* a, void* stream) {
+    if (!a || !a->x || !a->out || !a->ops || a->nops <= 0)
+        return fail(CGP_EINVAL, "var_chain: NULL pointer or empty op list");
+    if (a->n1 <= 0 || a->n2 < 0 || (a->n2 > 0 && !a->y) || a->channels <= 0 || a->h <= 0 ||
+        a->w <= 0 || a->store_total <= 0)
+        return fail(CGP_EINVAL, "var_chain: bad sizes");
+    const long long lds = (long long)a->lds_elems * (long long)sizeof(T);
+    if (a->lds_elems <= 0 || lds > 64 * 1024)
+        return fail(CGP_EINVAL, "var_chain: LDS footprint %lld bytes out of range", lds);
+    VarChainP<T> p;
+    p.x = static_cast<const T*>(a->x);
+    p.y = static_cast<const T*>(a->y ? a->y : a->x);
+    p.out = static_cast<T*>(a->out);
+    p.ops = a->ops;
+    p.n1 = a->n1;
+    p.n2 = a->n2;
+    p.store_total = a->store_total;
+    p.nops = a->nops;
+    p.channels = a->channels;
+    p.hw_in = a->h * a->w;
+    p.lds_elems = a->lds_elems;
+    p.scratch = a->scratch;
+    if (a->scratch < 0 || a->scratch >= a->lds_elems)
+        return fail(CGP_EINVAL, "var_chain: scratch offset out of range");
+    const long long n = a->n1 + a->n2;
+    const long long grid = n < 65536 ? n : 65536;
+    hipLaunchKernelGGL((var_chain_kernel<T>), dim3((unsigned)grid), dim3(kBlock), (size_t)lds,
+                       as_stream(stream), p);
+    return check_launch("var_chain_kernel");
+}
+
 __global__ __launch_bounds__(kBlock) void argmax_rows_kernel(const double* __restrict__ a,
                                                              long long rows, long long cols,
                                                              long long* __restrict__ out) {
@@ -1164,6 +1281,10 @@ int cgp_abi_version(void) { return CGP_ABI_VERSION; }
 const char* cgp_last_error(void) { return g_last_error.c_str(); }
 size_t cgp_conv_args_size(void) { return sizeof(cgp_conv_args); }
 size_t cgp_relu_args_size(void) { return sizeof(cgp_relu_args); }
+size_t cgp_var_op_size(void) { return sizeof(cgp_var_op); }
+size_t cgp_var_args_size(void) { return sizeof(cgp_var_args); }
+int cgp_var_chain_f64(const cgp_var_args* a, void* stream) { return var_chain_impl<double>(a, stream); }
+int cgp_var_chain_f32(const cgp_var_args* a, void* stream) { return var_chain_impl<float>(a, stream); }
 
 int cgp_selftest(void) {
     // FastDiv against exact division: every divisor the kernels use, edge numerators

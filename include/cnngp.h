@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 6
+#define CGP_ABI_VERSION 7
 
 /* error codes */
 #define CGP_OK 0
@@ -296,6 +296,53 @@ typedef struct cgp_net_args {
     int32_t program;       /* 0: interpret the op records; k > 0: run compiled program k,
                               the value cgp_net_program() returned for these records */
 } cgp_net_args;
+
+/*
+ * The per-image variance maps of a network in ONE launch (replaces the layer-by-layer
+ * variance pipeline of cnn_gp/program.py Plan.run_variances: one launch per op).  A self
+ * pair's recursion is linear (kernels.py:44-49 moments of x with itself, :92-98 convs,
+ * :154-164 the ReLU of a variance is xx/2, :252-254 Sums), so one workgroup walks an image
+ * through the whole op list in LDS and stores the maps the whole-network kernel reads.
+ *   CGP_VAR_MOMENTS  dst = mean_c x·x                       (src unused)
+ *   CGP_VAR_CONV     dst = w·Σ_window src + b   (zero padding; row sums, then columns)
+ *   CGP_VAR_HALF     dst = src / 2
+ *   CGP_VAR_SUM      dst = c0·t0 (+ c_k·t_k, k = 1..3, left to right; term slot -1 ends)
+ * A value is stored when store >= 0: image g's map at out[n·store + g·ho·wo] (n = n1 + n2
+ * images, the x images first), and, for g < n1, 0.25 × the map at
+ * out[n·store_total + n1·qstore + g·ho·wo] when qstore >= 0 (the quartered x-side maps of
+ * cgp_net_f64; store_total = Σ of every stored value's ho·wo).  Slots are LDS element
+ * offsets, maps row-major [ho][wo].
+ */
+#define CGP_VAR_MOMENTS 0
+#define CGP_VAR_CONV 1
+#define CGP_VAR_HALF 2
+#define CGP_VAR_SUM 3
+typedef struct cgp_var_op {
+    int32_t kind;
+    int32_t dst;
+    int32_t src[4];        /* CONV / HALF: src[0]; SUM: terms, -1 after the last */
+    int32_t h, w, ho, wo;  /* input and output map sizes */
+    int32_t taps, offset, stride, dilation;   /* CONV, as cgp_conv_args */
+    int64_t store;         /* per-image element offset of the stored map, -1: not stored */
+    int64_t qstore;        /* ... of its quartered x-side copy, -1: none */
+    double weight, bias;   /* CONV */
+    double coef[4];        /* SUM */
+} cgp_var_op;
+typedef struct cgp_var_args {
+    const void* x;         /* images [n1][channels][h][w] */
+    const void* y;         /* images [n2][channels][h][w] (n2 = 0: x only, e.g. same tiles) */
+    void* out;             /* stored maps, see above */
+    const cgp_var_op* ops; /* DEVICE array of nops ops */
+    int64_t n1, n2;
+    int64_t store_total;   /* Σ ho·wo of the stored values */
+    int32_t nops, channels, h, w;
+    int32_t lds_elems;     /* LDS of one image (elements of the compute type), scratch incl. */
+    int32_t scratch;       /* LDS offset of the convs' row-sum scratch ([h][wo] elements) */
+} cgp_var_args;
+size_t cgp_var_op_size(void);
+size_t cgp_var_args_size(void);
+int cgp_var_chain_f64(const cgp_var_args* args, void* stream);
+int cgp_var_chain_f32(const cgp_var_args* args, void* stream);
 
 /* Geometry code of a conv for CGP_NET_CONV, or -1 if the fused kernel has no
  * instantiation for it (the caller then runs the layer-by-layer path). */

@@ -712,3 +712,55 @@ def test_scale_batch_quarters_every_buffer():
     N.call("cgp_scale_batch_f64", k, ps, pd, pn, 0.25, stream())
     for s, d in zip(src, dst):
         assert torch.equal(d, s * 0.25)
+
+
+def _layer_variances(plan, x, y, n1, n2, same, need):
+    """the layer-by-layer variance pipeline (one launch per op) as the reference result"""
+    h, w = x.shape[2], x.shape[3]
+    var0 = torch.empty((n1 + n2, h, w), dtype=x.dtype, device=DEV)
+    sfx = "f64" if x.dtype == torch.float64 else "f32"
+    N.call(f"cgp_moments_var_{sfx}", N.ptr(x), N.ptr(y), n1, n2, x.shape[1], h * w,
+           N.ptr(var0[:n1]), N.ptr(var0[n1:]), stream())
+    return plan.run_variances(var0[:n1], var0[n1:], n1, n2, same, stream(), need=need)
+
+
+@pytest.mark.parametrize("cfg", CFGS + ["mixture"])
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+@pytest.mark.parametrize("same", [False, True])
+def test_var_chain_matches_layer_pipeline(cfg, dt, same):
+    """cgp_var_chain_* (every variance map of the network in one launch) against the
+    layer-by-layer variance pipeline it replaces: same values up to summation order
+    (separable window sums in both), quartered x-side copies exactly v/4, yy aliasing xx
+    on same tiles"""
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    if cfg == "mixture":
+        model, side = configs_util.mixture_nets()["big"]
+        C = 1
+    else:
+        model = configs_util.model(cfg)
+        C = 3 if cfg == "cifar10" else 1
+        side = 32 if C == 3 else 28
+    model = model.to(DEV, tdt)
+    g = torch.Generator().manual_seed(11)
+    n1, n2 = 5, 3
+    x = torch.rand((n1, C, side, side), generator=g, dtype=tdt).to(DEV)
+    y = x if same else torch.rand((n2, C, side, side), generator=g, dtype=tdt).to(DEV)
+    m2 = n1 if same else n2
+    plan = model._plan(side, side)
+    need = set(range(plan.prog.n_values))          # every value, not only the ReLU inputs
+    quarter = set(list(need)[::3])
+    got = plan.run_variances_fused(x, y, n1, m2, same, stream(), need, quarter)
+    assert got is not None
+    var, qvar = got
+    ref = _layer_variances(plan, x, y, n1, m2, same, need)
+    tol = 1e-13 if dt == "f64" else 2e-6
+    assert set(var) == set(ref)
+    for v in ref:
+        for a, b in zip(var[v], ref[v]):
+            a, b = a.double().cpu(), b.double().cpu()
+            assert a.shape == b.shape
+            assert torch.allclose(a, b, rtol=tol, atol=0), (v, float((a - b).abs().max()))
+    if same:
+        assert all(var[v][1].data_ptr() == var[v][0].data_ptr() for v in var)
+    for v, q in qvar.items():
+        assert torch.equal(q, var[v][0] * 0.25)
