@@ -468,7 +468,9 @@ class Plan:
         need = set(need)
         quarter = set(quarter) & need
         chain = self._var_chain(need, quarter, x.device)
-        if chain is None or chain["lds"] * x.element_size() > 64 * 1024:
+        # the chain kernel holds maps of up to 4·256 pixels per workgroup in 64 KB of LDS
+        if chain is None or chain["lds"] * x.element_size() > 64 * 1024 or \
+                x.shape[2] * x.shape[3] > 1024:
             return None
         m2 = 0 if same else n2
         n = n1 + m2

@@ -42,7 +42,7 @@ inline hipError_t stream_device(hipStream_t s, int* dev) {
 struct FastDiv {
     unsigned m, s, d;
 };
-inline FastDiv make_fastdiv(unsigned d) {
+__host__ __device__ inline FastDiv make_fastdiv(unsigned d) {
     FastDiv f;
     f.d = d;
     f.s = 0;

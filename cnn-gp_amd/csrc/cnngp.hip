@@ -784,20 +784,31 @@ struct VarChainP {
     long long n1, n2, store_total;
     int nops, channels, hw_in, lds_elems, scratch;
 };
+// Barriers are LDS-only (lds_barrier: wait for this wave's LDS traffic, not its global
+// stores): a stored map's LDS reads have returned before its global stores issue, so a
+// later op may overwrite the slot while the stores drain.
+// op records through the constant address space: every field is uniform, so they load
+// with scalar loads into SGPRs (a generic pointer gets per-lane vector loads, and a local
+// copy of the record indexed at run time would live in scratch memory)
+typedef const __attribute__((address_space(4))) cgp_var_op* VarOpsC;
+constexpr int kVarE = 4;   // map pixels per thread (maps up to 4·kBlock = 32x32)
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void var_chain_kernel(const VarChainP<T> p) {
     extern __shared__ __align__(16) unsigned char var_smem[];
     T* lds = reinterpret_cast<T*>(var_smem);
+    const VarOpsC ops = (VarOpsC)p.ops;
     const long long n = p.n1 + p.n2;
+    const int tid = threadIdx.x;
     for (long long g = blockIdx.x; g < n; g += gridDim.x) {
         const T* img = g < p.n1 ? p.x + g * p.channels * p.hw_in
                                 : p.y + (g - p.n1) * p.channels * p.hw_in;
         for (int k = 0; k < p.nops; ++k) {
-            const cgp_var_op op = p.ops[k];
-            const int howo = op.ho * op.wo;
-            T* dst = lds + op.dst;
-            if (op.kind == CGP_VAR_MOMENTS) {
-                for (int e = threadIdx.x; e < howo; e += kBlock) {
+            const int kind = ops[k].kind;
+            const int ho = ops[k].ho, wo = ops[k].wo, howo = ho * wo;
+            T* dst = lds + ops[k].dst;
+            if (kind == CGP_VAR_MOMENTS) {
+                for (int e = tid; e < howo; e += kBlock) {
                     T acc = img[e] * img[e];
                     for (int c = 1; c < p.channels; ++c) {
                         const T v = img[(size_t)c * p.hw_in + e];
@@ -805,51 +816,87 @@ __global__ __launch_bounds__(kBlock) void var_chain_kernel(const VarChainP<T> p)
                     }
                     dst[e] = acc / T(p.channels);
                 }
-            } else if (op.kind == CGP_VAR_CONV) {
+            } else if (kind == CGP_VAR_CONV) {
                 // separable like the layer kernels: window sums along each input row into
                 // the scratch, then along columns (a full-window conv stays parallel)
-                const T* src = lds + op.src[0];
+                const T* src = lds + ops[k].src[0];
                 T* hs = lds + p.scratch;
-                const T w = (T)op.weight, b = (T)op.bias;
-                for (int e = threadIdx.x; e < op.h * op.wo; e += kBlock) {
-                    const int r = e / op.wo, co = e - r * op.wo;
-                    T acc = T(0);
-                    for (int dx = 0; dx < op.taps; ++dx) {
-                        const int c = co * op.stride + op.offset + dx * op.dilation;
-                        if (c >= 0 && c < op.w) acc += src[r * op.w + c];
-                    }
-                    hs[e] = acc;
+                const int h = ops[k].h, w = ops[k].w, taps = ops[k].taps;
+                const int off = ops[k].offset, st = ops[k].stride, dl = ops[k].dilation;
+                const T wt = (T)ops[k].weight, b = (T)ops[k].bias;
+                const FastDiv fwo = make_fastdiv((unsigned)wo);
+                // up to kVarE elements per thread (maps of at most kVarE·kBlock pixels),
+                // their window sums interleaved tap by tap (independent LDS chains)
+                int rr[kVarE], cc[kVarE];
+                bool ok[kVarE];
+                T acc[kVarE];
+#pragma unroll
+                for (int i = 0; i < kVarE; ++i) {
+                    const int e = tid + i * kBlock;
+                    ok[i] = e < h * wo;
+                    rr[i] = (int)fdiv((unsigned)(ok[i] ? e : 0), fwo);
+                    cc[i] = (ok[i] ? e : 0) - rr[i] * wo;
+                    acc[i] = T(0);
                 }
-                __syncthreads();
-                for (int e = threadIdx.x; e < howo; e += kBlock) {
-                    const int ro = e / op.wo, co = e - ro * op.wo;
-                    T acc = T(0);
-                    for (int dy = 0; dy < op.taps; ++dy) {
-                        const int r = ro * op.stride + op.offset + dy * op.dilation;
-                        if (r >= 0 && r < op.h) acc += hs[r * op.wo + co];
+                for (int dx = 0; dx < taps; ++dx) {
+#pragma unroll
+                    for (int i = 0; i < kVarE; ++i) {
+                        const int c = cc[i] * st + off + dx * dl;
+                        if (ok[i] && c >= 0 && c < w) acc[i] += src[rr[i] * w + c];
                     }
-                    dst[e] = w * acc + b;
                 }
-            } else if (op.kind == CGP_VAR_HALF) {
-                const T* src = lds + op.src[0];
-                for (int e = threadIdx.x; e < howo; e += kBlock) dst[e] = src[e] / T(2);
-            } else {   // CGP_VAR_SUM
-                for (int e = threadIdx.x; e < howo; e += kBlock) {
-                    T acc = (T)op.coef[0] * lds[op.src[0] + e];
-                    for (int t = 1; t < 4 && op.src[t] >= 0; ++t)
-                        acc = acc + (T)op.coef[t] * lds[op.src[t] + e];
+#pragma unroll
+                for (int i = 0; i < kVarE; ++i)
+                    if (ok[i]) hs[tid + i * kBlock] = acc[i];
+                lds_barrier();
+#pragma unroll
+                for (int i = 0; i < kVarE; ++i) {
+                    const int e = tid + i * kBlock;
+                    ok[i] = e < howo;
+                    rr[i] = (int)fdiv((unsigned)(ok[i] ? e : 0), fwo);
+                    cc[i] = (ok[i] ? e : 0) - rr[i] * wo;
+                    acc[i] = T(0);
+                }
+                for (int dy = 0; dy < taps; ++dy) {
+#pragma unroll
+                    for (int i = 0; i < kVarE; ++i) {
+                        const int r = rr[i] * st + off + dy * dl;
+                        if (ok[i] && r >= 0 && r < h) acc[i] += hs[r * wo + cc[i]];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < kVarE; ++i)
+                    if (ok[i]) dst[tid + i * kBlock] = wt * acc[i] + b;
+            } else if (kind == CGP_VAR_HALF) {
+                const T* src = lds + ops[k].src[0];
+                for (int e = tid; e < howo; e += kBlock) dst[e] = src[e] / T(2);
+            } else {   // CGP_VAR_SUM: c0·t0, then o + c_k·t_k (the axpby chain)
+                int sl[4];
+                T cf[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    sl[t] = ops[k].src[t];
+                    cf[t] = (T)ops[k].coef[t];
+                }
+                for (int e = tid; e < howo; e += kBlock) {
+                    T acc = cf[0] * lds[sl[0] + e];
+#pragma unroll
+                    for (int t = 1; t < 4; ++t)
+                        if (sl[t] >= 0) acc = acc + cf[t] * lds[sl[t] + e];
                     dst[e] = acc;
                 }
             }
-            __syncthreads();
-            if (op.store >= 0) {
-                T* o = p.out + n * op.store + g * howo;
-                for (int e = threadIdx.x; e < howo; e += kBlock) o[e] = dst[e];
-                if (op.qstore >= 0 && g < p.n1) {
-                    T* q = p.out + n * p.store_total + p.n1 * op.qstore + g * howo;
-                    for (int e = threadIdx.x; e < howo; e += kBlock) q[e] = T(0.25) * dst[e];
+            lds_barrier();
+            const long long sto = ops[k].store;
+            if (sto >= 0) {
+                T* o = p.out + n * sto + g * howo;
+                for (int e = tid; e < howo; e += kBlock) o[e] = dst[e];
+                const long long qs = ops[k].qstore;
+                if (qs >= 0 && g < p.n1) {
+                    T* q = p.out + n * p.store_total + p.n1 * qs + g * howo;
+                    for (int e = tid; e < howo; e += kBlock) q[e] = T(0.25) * dst[e];
                 }
-                __syncthreads();   // a later op may reuse the slot
+                lds_barrier();   // a later op may reuse the slot
             }
         }
     }
@@ -880,6 +927,8 @@ int var_chain_impl(const cgp_var_args* a, void* stream) {
     p.scratch = a->scratch;
     if (a->scratch < 0 || a->scratch >= a->lds_elems)
         return fail(CGP_EINVAL, "var_chain: scratch offset out of range");
+    if ((long long)a->h * a->w > (long long)kVarE * kBlock)
+        return fail(CGP_EINVAL, "var_chain: maps larger than %d pixels", kVarE * kBlock);
     const long long n = a->n1 + a->n2;
     const long long grid = n < 65536 ? n : 65536;
     hipLaunchKernelGGL((var_chain_kernel<T>), dim3((unsigned)grid), dim3(kBlock), (size_t)lds,
