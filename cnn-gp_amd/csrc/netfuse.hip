@@ -1072,6 +1072,12 @@ int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_ele
 #ifndef CGP_NET_DYN
 #define CGP_NET_DYN 1
 #endif
+#ifndef CGP_NET_XCD_PROBE
+#define CGP_NET_XCD_PROBE 0
+#endif
+#if CGP_NET_XCD_PROBE
+__device__ unsigned long long g_exit_clock[1 << 16];
+#endif
 // PID >= 0: compiled program PID instead of the op-record interpreter.
 template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
 __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
@@ -1227,6 +1233,11 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
         }
         lds_barrier();
     }
+#if CGP_NET_XCD_PROBE
+    // A/B builds: each workgroup's exit time (s_memrealtime, 100 MHz) for the per-XCD
+    // balance probe (tools/xcd_probe.py)
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) g_exit_clock[blockIdx.x] = wall_clock64();
+#endif
 }
 
 // waves per SIMD the LDS footprint of a workgroup allows (`waves` waves per workgroup,
@@ -1531,6 +1542,12 @@ int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t 
                       lds_elems, itemsize);
 }
 
+#if CGP_NET_XCD_PROBE
+int cgp_net_probe_read(unsigned long long* host, int32_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_exit_clock), sizeof(unsigned long long) * n) ==
+                   hipSuccess ? 0 : CGP_EHIP;
+}
+#endif
 int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }
 int cgp_net_f32(const cgp_net_args* args, void* stream) { return net_impl<float>(args, stream); }
 
