@@ -30,7 +30,7 @@ Also on the same JSON line:
                      is given, with the committed calibration against the reference
 
 Multi-GPU (one process per GPU, torchrun): the Kxx grows with the world
-(n_blocks·(n_blocks+1)/2 >= tiles_per_rank·world, work divisible evenly) and its tiles
+(n_blocks² half-tile units >= world × the 1-GPU units, divisible by world) and its tiles
 are split over the ranks by evaluated pairs — no data-path collective; per-rank work is
 ~constant ("scaling": "weak").  The full-scale leg shards its fixed problem ("strong")
 and gathers once per matrix.
@@ -88,15 +88,16 @@ def parse():
 
 
 def blocks_for_world(n1: int, tile: int, world: int) -> int:
-    """Smallest n_blocks whose upper-triangular tile count covers world × the 1-GPU one
-    and whose work splits evenly: in half-tile units (a diagonal tile evaluates half the
-    pairs of an off-diagonal one) nb blocks hold nb(nb−1) + nb = nb² units, so nb² must
-    divide by the world size (at 8 ranks 13 blocks would leave one rank 4% over the
-    mean; 16 blocks give every rank exactly 32 units)."""
+    """Smallest n_blocks whose evaluated work covers world × the 1-GPU work and splits
+    evenly.  Work is counted in half-tile units (a diagonal tile evaluates half the pairs
+    of an off-diagonal one): nb blocks hold nb(nb−1) + nb = nb² units, so nb² must reach
+    world · b1² and divide by the world size.  At B = 1024 that is 4 / 6 / 8 / 12 blocks
+    at N = 1 / 2 / 4 / 8, i.e. 16 / 18 / 16 / 18 units per rank (an earlier rule counted tiles
+    instead of units, which gave 16 / 18 / 25 / 32: per-rank work grew with N)."""
     b1 = -(-n1 // tile)
-    target = b1 * (b1 + 1) // 2 * world
+    target = b1 * b1 * world
     nb = b1
-    while nb * (nb + 1) // 2 < target or (world > 1 and (nb * nb) % world):
+    while nb * nb < target or (world > 1 and (nb * nb) % world):
         nb += 1
     return nb
 

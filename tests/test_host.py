@@ -350,6 +350,11 @@ def test_bench_balanced_split_covers_every_tile_once():
         # nb² divisible by the world size: every rank within a few pairs of the mean
         assert (nb * nb) % world == 0 or world == 1
         assert max(loads) <= sum(loads) / world * (1 + 1e-3), (world, loads)
+        # weak scaling: per-rank work stays within 1/8 of the 1-GPU work at N = 2, 4, 8
+        if world in (2, 4, 8):
+            assert sum(loads) / world <= sum(loads_1) * 1.126, (world, loads)
+        if world == 1:
+            loads_1 = loads
 
 
 # ------------------------------------------------------------------------------------
