@@ -335,6 +335,8 @@ def test_bench_balanced_split_covers_every_tile_once():
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     B = 1024
+    # the block counts DESIGN §7 quotes for the driver's N = 1 / 2 / 4 / 8 runs
+    assert [bench.blocks_for_world(4096, B, w) for w in (1, 2, 4, 8)] == [4, 6, 8, 12]
     for world in (1, 2, 3, 4, 8):
         nb = bench.blocks_for_world(4096, B, world)
         n = nb * B
