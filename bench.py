@@ -80,7 +80,10 @@ def parse():
     p.add_argument("--no-fullscale", action="store_true")
     p.add_argument("--no-fullscale-f32", action="store_true",
                    help="skip the float32-kernel repeat of the full-scale leg")
+    p.add_argument("--no-fullscale-cifar10", action="store_true",
+                   help="skip BASELINE configs[4]: cifar10 Kxx 50 000² + Kxz + solve")
     p.add_argument("--fullscale-n", type=int, default=60000)
+    p.add_argument("--cifar10-n", type=int, default=50000)
     p.add_argument("--fullscale-m", type=int, default=10000)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target duration of the CPU-baseline sample")
@@ -292,13 +295,50 @@ def cpu_info():
     return model
 
 
+def host_cpu_budget():
+    """CPU threads this process may use on the host: its affinity set, capped by a cgroup
+    CPU quota (cgroup v2 cpu.max, v1 cfs_quota) and by the pool's per-GPU CPU share when
+    the environment states one (OMP_NUM_THREADS: the GPU pool sets it to the box's share,
+    16 per GPU, while nproc / os.cpu_count() report the whole machine).  Returns (threads,
+    facts) — every number the choice was made from, for the bench line."""
+    facts = {"affinity": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count()}
+    quota = None
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            txt = open(path).read().strip()
+        except OSError:
+            continue
+        if parse:
+            q, per = parse(txt)
+            if q != "max":
+                quota = -(-int(q) // int(per))
+        else:
+            q = int(txt)
+            if q > 0:
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                quota = -(-q // per)
+        break
+    facts["cgroup_cpu_quota"] = quota
+    omp = os.environ.get("OMP_NUM_THREADS")
+    facts["OMP_NUM_THREADS"] = int(omp) if omp and omp.isdigit() else None
+    threads = facts["affinity"]
+    for cap in (quota, facts["OMP_NUM_THREADS"]):
+        if cap:
+            threads = min(threads, cap)
+    return max(1, threads), facts
+
+
 def cpu_baseline(cfg_name, dtype, seconds):
     """The torch-CPU restatement of the reference (oracle/torch_cpu.py — the reference's
-    op sequence, bit-identical to it at C1) on the host threads torch is given, on a Kxz
-    tile sized for about ``seconds`` of work after a small warm-up that measures the
-    rate.  The calibration restatement/reference measured in the build container
-    (tools/calibrate_cpu.py) is quoted beside it."""
+    op sequence, bit-identical to it at C1) on the host's CPU budget (host_cpu_budget:
+    affinity, cgroup quota, the pool's per-GPU share), on a Kxz tile sized for about
+    ``seconds`` of work after a small warm-up that measures the rate.  The calibration
+    restatement/reference measured in the build container (tools/calibrate_cpu.py) is
+    quoted beside it."""
     from oracle import specs, torch_cpu
+    threads, facts = host_cpu_budget()
+    torch.set_num_threads(threads)
     spec = specs.CONFIGS[cfg_name]()
     C, hw = specs.GEOMETRY[cfg_name]
     g = torch.Generator().manual_seed(0)
@@ -316,7 +356,9 @@ def cpu_baseline(cfg_name, dtype, seconds):
     el = time.perf_counter() - t0
     dtn = "f64" if dt == torch.float64 else "f32"
     res = dict(value=round(side * side / el, 1), unit="pairs/s", cores=torch.get_num_threads(),
-               kind="port", nproc=os.cpu_count(), cpu_model=cpu_info(),
+               kind="port", nproc=os.cpu_count(), cpu_model=cpu_info(), host_cpus=facts,
+               threads_rule="min(affinity, cgroup quota, OMP_NUM_THREADS = the pool's "
+                            "per-GPU CPU share)",
                sample=f"one {side}x{side} Kxz tile of {cfg_name} ({side * side} pairs, {dtn}) "
                       f"through oracle/torch_cpu.py (the reference's torch op sequence) "
                       f"in {el:.1f} s on {torch.get_num_threads()} threads")
@@ -460,6 +502,9 @@ def main():
                                        f"tiles {B}", "pairs_per_step": r2["evaluated"]},
                 "roofline": net_roofline(r2["model"], r2["X"][:B], "mnist_as_tf",
                                          r2["timing"]) if probe else None}
+            if world == 1 and not args.no_cpu:
+                extra["mnist_as_tf"]["cpu_baseline"] = cpu_baseline(
+                    "mnist_as_tf", dtype, args.cpu_seconds)
         torch.cuda.empty_cache()
 
     # --- the same two workloads at the reference pipeline's own kernel precision ---
@@ -513,6 +558,21 @@ def main():
                               "the float64 model (north-star tolerance 1e-5)")
                 extra["fullscale_f32"] = fs
             torch.cuda.empty_cache()
+
+    # --- BASELINE configs[4]: cifar10 ResNet-GP, Kxx 50 000² on 3×32×32 ---
+    if not args.no_fullscale_cifar10 and dtype == torch.float64:
+        from fullscale import fullscale
+        t0 = time.perf_counter()
+        fs = fullscale("cifar10", args.cifar10_n, args.fullscale_m, 4096, rank=rank,
+                       world=world, dev=dev)
+        if rank == 0:
+            fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
+            fs["data"] = "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)"
+            fs["note"] = ("BASELINE configs[4] (configs/cifar10.py:4-47 architecture): Kxx + "
+                          "Kxz 10 000 x N tiles (B=4096) split over the ranks, gathered to "
+                          "rank 0, rocSOLVER solve + predict there")
+            extra["fullscale_cifar10"] = fs
+        torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -138,6 +138,7 @@ SIGNATURES = {
     "cgp_net_geometry": (_i32, [_i32] * 7),
     "cgp_net_hs_elems": (_i32, [_i32]),
     "cgp_net_supertile": (_i32, []),
+    "cgp_net_units": (_i32, [_i32]),
     "cgp_net_resolution": (_i32, [_i32, _i32]),
     "cgp_net_op_size": (ctypes.c_size_t, []),
     "cgp_net_args_size": (ctypes.c_size_t, []),

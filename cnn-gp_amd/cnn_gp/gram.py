@@ -116,10 +116,12 @@ def _eval_tile(kern, X, src2, t: Tile):
 
 def gram_tiles(kern: Callable, X, X2=None, batch_size: int = 1024, worker_rank: int = 0,
                n_workers: int = 1, out: Optional[torch.Tensor] = None, device=None,
-               dtype=torch.float64, split: str = "reference"):
+               dtype=torch.float64, split: str = "balanced"):
     """Evaluate this worker's tiles into ``out`` ([N, N2], NaN where not computed; a new
     device matrix when None).  Returns (out, tiles) with tiles the (same, i0, j0, rows,
-    cols) written.  For one process; ranks of a group use ``gram_local``."""
+    cols) written.  For one process; ranks of a group use ``gram_local``.  ``split`` has
+    the same default as ``gram_local`` / ``gather_gram`` (with one worker both splits are
+    every tile)."""
     N = len(X)
     N2 = N if X2 is None else len(X2)
     src2 = X if X2 is None else X2
@@ -161,11 +163,13 @@ def _capacity(N, N2, batch_size, world, split):
 
 
 def gather_gram(local: torch.Tensor, N: int, N2: Optional[int], batch_size: int,
-                group=None, dst: int = 0, split: str = "balanced"):
+                group=None, dst: int = 0, split: Optional[str] = None):
     """Assemble every rank's tiles on rank ``dst`` with one gather.
 
-    ``local`` is this rank's flat buffer from ``gram_local`` (or, for compatibility, an
-    [N, N2] matrix holding its tiles — they are packed first).  Every rank's buffer is
+    ``local`` is this rank's flat buffer from ``gram_local`` (split default "balanced",
+    as there), or an [N, N2] matrix holding its tiles — packed first, which needs the
+    ``split`` the matrix was filled with named explicitly, and every packed tile must be
+    finite (a tile of another split's plan would still hold the NaN fill).  Every rank's buffer is
     padded to the largest share; rank ``dst`` unpacks them by the shared, deterministic
     tile plan into a NaN-filled [N, N2] matrix on ``local``'s device and returns it; the
     other ranks return None.  With a gloo group, device buffers travel through host
@@ -173,14 +177,22 @@ def gather_gram(local: torch.Tensor, N: int, N2: Optional[int], batch_size: int,
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n2 = N if N2 is None else N2
+    if local.dim() != 2 and split is None:
+        split = "balanced"                     # gram_local's default
     plans = [tile_plan(N, N2, batch_size, r, world, split) for r in range(world)]
     cap = max(1, max(sum(a * b for _, _, _, a, b in p) for p in plans))
     if local.dim() == 2:
+        if split is None:
+            raise ValueError("gather_gram of an [N, N2] matrix: pass the split its tiles "
+                             "were evaluated with (gram_tiles(..., split=...))")
         packed = torch.empty(cap, dtype=local.dtype, device=local.device)
         off = 0
         for _, i0, j0, a, b in plans[rank]:
             packed[off:off + a * b].view(a, b).copy_(local[i0:i0 + a, j0:j0 + b])
             off += a * b
+        if not bool(torch.isfinite(packed[:off]).all()):
+            raise ValueError(f"rank {rank}: a tile of the {split!r} plan is not finite in the "
+                             "matrix given — it was filled with another split")
         local = packed
     if local.numel() < cap:
         grown = torch.empty(cap, dtype=local.dtype, device=local.device)

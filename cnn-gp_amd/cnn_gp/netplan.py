@@ -118,8 +118,11 @@ def first_pairs(n_stages: int) -> int:
     return 2 if FIRST_PAIRS in ("2", "auto") else 1
 MIN_STAGE_OPS = 4                      # a shorter tail is not worth a launch + state
 # state buffers: units per launch group (each group runs every stage once, and each launch
-# ends in a tail where the last workgroups finish their pairs)
+# ends in a tail where the last workgroups finish their pairs).  The cap is also clamped
+# so that all of a tile's state buffers take at most STATE_FREE_FRAC of the device's free
+# memory (NetPlan.chunk_units)
 CHUNK_BYTES = int(os.environ.get("CGP_NET_CHUNK_MB", "8192")) << 20
+STATE_FREE_FRAC = 0.25
 
 
 class NetPlan:
@@ -196,7 +199,8 @@ class NetPlan:
             outs = sorted(v for v, pi in prod.items() if pi < hi <= last.get(v, -1)) \
                 if hi < len(lowered) else []
             st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
-            if np_ == 2 and st.lds_elems * itemsize * 2 > MAX_LDS_BYTES:
+            # the two-pair workgroup holds cgp_net_units(2) one-pair arenas (CGP_NET_SPLIT)
+            if np_ == 2 and st.lds_elems * itemsize * lib.cgp_net_units(2) > MAX_LDS_BYTES:
                 st = self._lower(lowered, lo, hi, 1, ins, outs, last, dual, itemsize)
             self.stages.append(st)
         self.need_var = {vf}
@@ -495,7 +499,7 @@ class NetPlan:
                 f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
             elif f["kind"] in (N.CGP_NET_MOMENTS, N.CGP_NET_LINEAR):
                 f["code"] = -1
-        if top * itemsize * pairs > MAX_LDS_BYTES:
+        if top * itemsize * lib.cgp_net_units(pairs) > MAX_LDS_BYTES:
             if pairs == 1:
                 raise Unsupported(f"LDS footprint {top * itemsize} B")
         return Stage(records=recs, lds_elems=top, final_slot=final_origin, pairs=pairs,
@@ -530,6 +534,18 @@ class NetPlan:
                 o.var_x = state_out.data_ptr()
         return arr
 
+    def chunk_units(self, itemsize: int, units: int, device=None) -> int:
+        """Units per launch group of a staged program: CHUNK_BYTES of the widest state
+        record, clamped so that the state buffers of every stage boundary together take at
+        most STATE_FREE_FRAC of the device's free memory; a multiple of 64, at least 64."""
+        stride = max(max(st.load_stride, st.store_stride) for st in self.stages)
+        chunk = CHUNK_BYTES // (stride * itemsize)
+        if device is not None and torch.device(device).type == "cuda":
+            free = torch.cuda.mem_get_info(device)[0]
+            per_unit = sum(st.load_stride for st in self.stages[1:]) * itemsize
+            chunk = min(chunk, int(free * STATE_FREE_FRAC) // max(1, per_unit))
+        return min(max(64, chunk // 64 * 64), units)
+
     @staticmethod
     def units(n1: int, n2: int, same: bool) -> int:
         """Pair units of a tile: st x st supertiles (upper triangle when same) x st²,
@@ -555,9 +571,7 @@ class NetPlan:
         chunk = units
         states = [None] * (len(self.stages) + 1)
         if multi:
-            stride = max(max(st.load_stride, st.store_stride) for st in self.stages)
-            chunk = max(64, CHUNK_BYTES // (stride * x.element_size()) // 64 * 64)
-            chunk = min(chunk, units)
+            chunk = self.chunk_units(x.element_size(), units, x.device)
             for b in range(1, len(self.stages)):
                 states[b] = torch.empty((chunk * self.stages[b].load_stride,),
                                         dtype=x.dtype, device=x.device)

@@ -425,7 +425,11 @@ class Plan:
         recs.append(r)
         for idx, op in enumerate(ops):
             srcs = [op.src] if op.kind in ("conv", "relu") else [t for _, t in op.terms]
-            if len(srcs) > 4:
+            # the chain kernel covers at most kVarE·kBlock = 1024 elements per pass, over
+            # both the row pass (h·wo) and the output (ho·wo): a conv padded beyond "same"
+            # grows its map past the input's, so the input size alone does not bound it
+            (hi_, wi_), (ho_, wo_) = shapes[srcs[0]], op.shape_out
+            if len(srcs) > 4 or max(hi_ * wo_, ho_ * wo_, hi_ * wi_) > 1024:
                 cache[key] = None
                 return None
             r = N.VarOp(dst=alloc(op.dst))

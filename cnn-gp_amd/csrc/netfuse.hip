@@ -1524,6 +1524,8 @@ size_t cgp_net_args_size(void) { return sizeof(cgp_net_args); }
 
 int cgp_net_supertile(void) { return kST; }
 
+int cgp_net_units(int32_t pairs) { return net_units(pairs <= 0 ? 1 : pairs); }
+
 int cgp_net_hs_elems(int32_t code) {
     return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;
 }

@@ -363,6 +363,10 @@ int cgp_net_resolution(int32_t h, int32_t w);
 /* workgroups per CU the fused kernel reaches with lds_bytes of LDS per pair and `pairs`
  * pairs per workgroup (0 if it cannot run) */
 int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs);
+/* LDS arenas (one per pair unit) a workgroup of `pairs` pairs holds: `pairs`, except for
+ * the two-pair head stage, whose workgroup holds CGP_NET_SPLIT one-pair slices (2 in the
+ * default build).  A stage needs lds_bytes × cgp_net_units(pairs) <= 160 KB. */
+int cgp_net_units(int32_t pairs);
 /* The compiled program (k > 0) whose op list equals ops[0, nops) (HOST memory) in every
  * field but weight, bias and the variance / state pointers, for `pairs` pairs per
  * workgroup, flags (CGP_FLAG_NET_DUAL), the per-pair LDS footprint and the item size

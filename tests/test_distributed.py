@@ -41,8 +41,15 @@ def _worker(rank, world, port, X, Z, B, q):
         for name, X2 in (("Kxx", None), ("Kxz", Z)):
             n2 = None if X2 is None else len(X2)
             # legacy: a full matrix per rank, reference split
-            local, _ = gram_tiles(kern, X, X2, B, rank, world, device="cpu")
+            local, _ = gram_tiles(kern, X, X2, B, rank, world, device="cpu",
+                                  split="reference")
             full = gather_gram(local, len(X), n2, B, split="reference")
+            # a matrix needs its split named; one filled by another plan is refused
+            with pytest.raises(ValueError):
+                gather_gram(local, len(X), n2, B)
+            if world == 3 and rank == 2 and X2 is None:   # its plans differ (4, 4)
+                with pytest.raises(ValueError, match="not finite"):
+                    gather_gram(local, len(X), n2, B, split="balanced")
             # packed: only this rank's tiles, balanced split
             buf, tiles = gram_local(kern, X, X2, B, rank, world, device="cpu")
             assert buf.numel() == sum(a * b for *_, a, b in tiles)

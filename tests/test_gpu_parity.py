@@ -764,3 +764,25 @@ def test_var_chain_matches_layer_pipeline(cfg, dt, same):
         assert all(var[v][1].data_ptr() == var[v][0].data_ptr() for v in var)
     for v, q in qvar.items():
         assert torch.equal(q, var[v][0] * 0.25)
+
+
+def test_var_chain_rejects_maps_grown_by_padding():
+    """A conv padded beyond "same" grows its map past the input's (1x1, padding 2 on 30x30
+    gives 34x34 = 1156 pixels): the one-launch variance chain covers at most 1024 pixels
+    per pass, so it must decline (None) and the forward must take the layer path —
+    and still match the oracle."""
+    m = cnn_gp.Sequential(cnn_gp.Conv2d(1, padding=2, var_weight=1.3, var_bias=0.2),
+                          cnn_gp.ReLU(), cnn_gp.Conv2d(34, padding=0, var_weight=2.0))
+    m = m.to(DEV, torch.float64)
+    spec = specs.seq(specs.conv(1, padding=2, var_weight=1.3, var_bias=0.2), specs.RELU,
+                     specs.conv(34, padding=0, var_weight=2.0))
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand((3, 1, 30, 30), generator=g, dtype=torch.float64)
+    y = torch.rand((2, 1, 30, 30), generator=g, dtype=torch.float64)
+    plan = m._plan(30, 30)
+    need = set(range(plan.prog.n_values))
+    assert plan.run_variances_fused(x.to(DEV), y.to(DEV), 3, 2, False, stream(), need) is None
+    with torch.no_grad():
+        got = m(x.to(DEV), y.to(DEV), False, False).cpu().numpy()
+    ref = O.kernel(spec, x.numpy(), y.numpy(), False, False)
+    assert rel_err(got, ref) < RTOL64["fast"]

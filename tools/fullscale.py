@@ -167,7 +167,10 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
             worst = max(worst, abs(K[a, b].item() - ref) / abs(ref))
             ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
             worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
-    res["spot_check_max_rel_err"] = worst
+    # HIP against HIP: the same drop-in call on single pairs (other tile shapes, no
+    # chunking) — a self-consistency check; parity with the CPU oracle at this tile
+    # geometry is tests/test_gpu_fullgeom.py
+    res["spot_check_hip_vs_hip_max_rel_err"] = worst
     if kd != torch.float64:
         # the float32 entries against the float64 model on the same (exactly widened)
         # images: the north star's 1e-5 relative tolerance
