@@ -233,3 +233,163 @@ def gram_matrix(model, X, X2=None, batch_size: int = 1024, device=None,
         return gather_gram(local, N, N2, batch_size, group, split=split)
     out, _ = gram_tiles(kern, X, X2, batch_size, device=device, dtype=dtype)
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Row strips: the full-scale layout (one contiguous block of rows per rank)
+# ------------------------------------------------------------------------------------------
+# A rank owns rows [r0, r1) of the matrix and evaluates every tile of them: for Kxx the
+# upper triangle of those rows (j >= i: its square [r0, r1)² as diagonal + upper tiles, then
+# the rectangle [r0, r1) × [r1, N)); for Kxz all of [r0, r1) × [0, N2) — the north star's
+# "row-blocks of X against all Z".  Rows i0:i1 of a row-major [N, N2] matrix are one
+# contiguous range, so rank 0 receives each rank's strip straight into its place in the
+# full matrix (one point-to-point receive per rank, all in flight together over xGMI): no
+# staging buffer, no unpack, and rank 0 evaluates its own strip in place — its peak is the
+# matrix itself (1.0× Kxx, against 2.1× for gather_gram's padded receive list).
+#
+# Strip boundaries come from the evaluated pairs: row i of Kxx costs N − 1 − i pairs (the
+# kernel evaluates i < j; K[i, i] is the variance chain's), a Kxz row costs N2, so the split
+# balances to one alignment unit of rows (8 = the kernel's supertile edge), not to one tile.
+# ``weights`` gives ranks unequal shares (e.g. a smaller Kxz share for the rank that
+# solves while the others build Kxz).
+
+def _row_cost_prefix(N: int, N2: Optional[int], r: int) -> int:
+    """evaluated pairs in rows [0, r)"""
+    if N2 is None:
+        return r * (N - 1) - r * (r - 1) // 2
+    return r * N2
+
+
+def strip_plan(N: int, N2: Optional[int], world: int, weights=None,
+               align: int = 8) -> List[Tuple[int, int]]:
+    """[(r0, r1)] per rank: contiguous row ranges covering [0, N) whose evaluated pairs
+    follow ``weights`` (default equal), boundaries on multiples of ``align``."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    w = [1.0] * world if weights is None else [float(v) for v in weights]
+    if len(w) != world or min(w) < 0 or sum(w) <= 0:
+        raise ValueError(f"weights {weights!r} for world {world}")
+    total = _row_cost_prefix(N, N2, N)
+    cuts, acc = [0], 0.0
+    for k in range(world - 1):
+        acc += w[k]
+        target = total * acc / sum(w)
+        lo, hi = cuts[-1], N                   # smallest r with prefix(r) >= target
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if _row_cost_prefix(N, N2, mid) >= target:
+                hi = mid
+            else:
+                lo = mid + 1
+        r = lo
+        if align > 1 and 0 < r < N:            # nearest aligned row
+            down = r // align * align
+            up = min(N, down + align)
+            r = down if target - _row_cost_prefix(N, N2, down) <= \
+                _row_cost_prefix(N, N2, up) - target else up
+        cuts.append(max(cuts[-1], min(N, r)))
+    cuts.append(N)
+    return [(cuts[k], cuts[k + 1]) for k in range(world)]
+
+
+def strip_cost(N: int, N2: Optional[int], rows: Tuple[int, int]) -> int:
+    """pairs the kernel evaluates for the strip ``rows``"""
+    return _row_cost_prefix(N, N2, rows[1]) - _row_cost_prefix(N, N2, rows[0])
+
+
+def strip_tiles(N: int, N2: Optional[int], rows: Tuple[int, int],
+                batch_size: int) -> List[Tile]:
+    """The tiles (same, i0, j0, a, b) of a strip, global coordinates.  Kxx: the square
+    [r0, r1)² in the reference's upper-tile order (data.py:22-29) with B-tiles anchored at
+    r0, then the rectangle [r0, r1) × [r1, N) in row blocks of B × B.  Kxz: [r0, r1) × [0, N2)
+    in B × B tiles.  For one strip covering [0, N) this is exactly tile_plan's list."""
+    r0, r1 = rows
+    B = batch_size
+    out: List[Tile] = []
+    if r1 <= r0:
+        return out
+    if N2 is not None:
+        for i0 in range(r0, r1, B):
+            for j0 in range(0, N2, B):
+                out.append((False, i0, j0, min(B, r1 - i0), min(B, N2 - j0)))
+        return out
+    for i0 in range(r0, r1, B):
+        a = min(B, r1 - i0)
+        out.append((True, i0, i0, a, a))
+        for j0 in range(i0 + B, r1, B):
+            out.append((False, i0, j0, a, min(B, r1 - j0)))
+        for j0 in range(r1, N, B):
+            out.append((False, i0, j0, a, min(B, N - j0)))
+    return out
+
+
+def gram_strip(kern: Callable, X, X2=None, batch_size: int = 4096,
+               rows: Tuple[int, int] = (0, 0), out: Optional[torch.Tensor] = None,
+               device=None, dtype=torch.float64):
+    """Evaluate the strip ``rows`` of Kxx (X2 None) or Kxz into ``out`` ([r1 − r0, N2] —
+    e.g. a row range of the full matrix; a new NaN-filled device block when None).  Entries
+    the strip does not evaluate (Kxx's strictly-lower part) stay as ``out`` had them.
+    Returns (out, tiles, pairs evaluated)."""
+    N = len(X)
+    N2 = None if X2 is None else len(X2)
+    n2 = N if N2 is None else N2
+    src2 = X if X2 is None else X2
+    r0, r1 = rows
+    if out is None:
+        out = torch.full((r1 - r0, n2), float("nan"), dtype=dtype,
+                         device=_default_device(device))
+    if tuple(out.shape) != (r1 - r0, n2):
+        raise ValueError(f"out {tuple(out.shape)} for strip rows {rows} of width {n2}")
+    tiles = strip_tiles(N, N2, rows, batch_size)
+    for t in tiles:
+        _, i0, j0, a, b = t
+        out[i0 - r0:i0 - r0 + a, j0:j0 + b].copy_(_eval_tile(kern, X, src2, t))
+    return out, tiles, sum(tile_cost(t) for t in tiles)
+
+
+def _p2p_staged(group, tensor_device) -> bool:
+    """gloo moves CPU tensors only: device buffers travel through host memory"""
+    return tensor_device.type == "cuda" and dist.get_backend(group) == "gloo"
+
+
+def gather_strips(strip: Optional[torch.Tensor], plan: List[Tuple[int, int]], n2: int,
+                  full: Optional[torch.Tensor] = None, group=None, dst: int = 0):
+    """Assemble every rank's strip on rank ``dst``: rank r sends its [r1 − r0, n2] block,
+    ``dst`` receives it straight into ``full[r0:r1]`` (a contiguous range of the row-major
+    matrix).  ``full`` on ``dst``: the [N, n2] matrix whose own rows already hold dst's
+    strip (gram_strip(out=full[r0:r1])).  All receives are posted together
+    (batch_isend_irecv: one link per peer over xGMI with RCCL); under gloo, device data is
+    staged through host memory one strip at a time.  Returns ``full`` on dst, None
+    elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(plan) != world:
+        raise ValueError(f"plan has {len(plan)} strips for world {world}")
+    if rank == dst:
+        if full is None or full.dim() != 2 or full.shape[1] != n2 or \
+                full.shape[0] != plan[-1][1] or not full.is_contiguous():
+            raise ValueError("dst needs the contiguous [N, n2] matrix holding its own strip")
+        peers = [(r, plan[r]) for r in range(world) if r != dst and plan[r][1] > plan[r][0]]
+        if _p2p_staged(group, full.device):
+            for r, (a, b) in peers:
+                buf = torch.empty((b - a, n2), dtype=full.dtype)
+                dist.recv(buf, dist.get_global_rank(group, r) if group else r, group=group)
+                full[a:b].copy_(buf)
+        elif peers:
+            ops = [dist.P2POp(dist.irecv, full[a:b], dist.get_global_rank(group, r)
+                              if group else r, group) for r, (a, b) in peers]
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return full
+    a, b = plan[rank]
+    if b > a:
+        if strip is None or tuple(strip.shape) != (b - a, n2):
+            raise ValueError(f"rank {rank}: strip must be [{b - a}, {n2}]")
+        peer = dist.get_global_rank(group, dst) if group else dst
+        if _p2p_staged(group, strip.device):
+            dist.send(strip.contiguous().cpu(), peer, group=group)
+        else:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, strip.contiguous(),
+                                                          peer, group)]):
+                req.wait()
+    return None

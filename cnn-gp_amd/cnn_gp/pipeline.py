@@ -1,0 +1,197 @@
+"""The exp_mnist_resnet pipeline over one process per GPU, in device memory.
+
+Reference: exp_mnist_resnet/run.bash:28-43 launches one save_kernel.py process per GPU
+(each writes its share of the Kxx / Kxvx tiles to its own HDF5 file), merge_h5_files.py
+NaN-merges the files, and classify_gp.py:61-77 loads Kxx, solves Kxx⁻¹Y and predicts
+argmax(Kxz @ A).  Here:
+
+1. every rank evaluates its row strip of Kxx (gram.strip_plan: balanced by evaluated
+   pairs to 8 rows; gram.gram_strip), rank ``dst`` straight into the full matrix;
+2. the strips are received into the full matrix on ``dst`` (gram.gather_strips: one
+   point-to-point receive per rank, all posted together — RCCL over xGMI);
+3. ``dst`` solves (rocSOLVER, classify_gp.py:17-27) WHILE the other ranks evaluate their
+   row strips of Kxz; ``dst`` takes a smaller Kxz share sized so that its solve plus its
+   strip ends with the others' strips (the solve time is estimated from n³/3 at
+   ``solve_tflops``, the kernel rate from the Kxx phase);
+4. α = Kxx⁻¹Y is broadcast, each rank multiplies its own Kxz rows by it, and only the
+   [m, classes] scores travel back to ``dst`` (Kxz itself is gathered only
+   when asked, e.g. for the HDF5 drop-in output or the posterior variance).
+
+With world size 1 the same function runs the four steps in order on one device.  The
+kernel, the solve and the score product are parameters, so the CPU tests drive this
+exact code with the oracle on gloo ranks.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+from .gram import gather_strips, gram_strip, strip_cost, strip_plan
+
+__all__ = ("classify_distributed", "kxz_weights")
+
+
+def kxz_weights(world: int, n: int, m: int, kernel_pairs_per_s: float,
+                solve_tflops: float = 30.0, dst: int = 0):
+    """Kxz row shares: rank ``dst`` also solves, so its share s0 satisfies
+    solve + s0·T = (1 − s0)/(world − 1)·T, T = m·n / rate (the whole Kxz on one GPU),
+    clipped to [0, 1/world].  None (equal shares) at world size 1."""
+    if world <= 1:
+        return None
+    T = m * n / max(kernel_pairs_per_s, 1.0)
+    S = n ** 3 / 3.0 / (solve_tflops * 1e12)
+    s0 = (T / (world - 1) - S) / (T + T / (world - 1))
+    s0 = min(max(s0, 0.0), 1.0 / world)
+    w = [(1.0 - s0) / (world - 1)] * world
+    w[dst] = s0
+    return w
+
+
+def _bcast(t: torch.Tensor, src: int, group):
+    if t.device.type == "cuda" and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.broadcast(h, src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src, group=group)
+    return t
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
+                         scores: Callable, batch_size: int = 4096, group=None, dst: int = 0,
+                         device=None, dtype=torch.float64, out_dtype=torch.float64,
+                         gather_kxz: bool = False, kxz_share=None, solve_tflops: float = 30.0,
+                         widen: Optional[Callable] = None, log: Optional[Callable] = None):
+    """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
+    group (or one process).
+
+    kern(x, x2, same) -> [a, b] tile (gram.model_kern); solve(K, Y) -> α (may factor K in
+    place, e.g. solve_system(..., overwrite_a=True)); scores(Kz, α) -> [rows, classes].
+    ``dtype``: the kernel's output dtype (K is stored in it; float32 as the reference's
+    save_kernel.py stores it); ``out_dtype``: the dtype solve and scores receive (float64:
+    classify_gp.py:45-48 widens K) — ``widen(t)`` converts (default ``t.to(out_dtype)``;
+    it may release its input).  Returns on ``dst`` a dict with alpha, scores, pred, K (the
+    matrix solve saw), Kxz (when gather_kxz), dst's own Kxz rows (``kxz_rows``,
+    ``Kxz_rows``), timings, the plans and the device memory peaks (overall, and from the
+    end of the Kxx build: the gather, the solve and the Kxz phase); None on the other
+    ranks."""
+    conv = widen or (lambda t: t.to(out_dtype))
+    dev = torch.device(device) if device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+        else torch.device("cpu"))
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    world = dist.get_world_size(group) if multi else 1
+    rank = dist.get_rank(group) if multi else 0
+    n, m = len(X), len(Z)
+    say = log if (log is not None and rank == dst) else (lambda *_: None)
+    res = {"world": world}
+
+    # 1. Kxx strips (dst evaluates its rows in place in the full matrix)
+    plan_x = strip_plan(n, None, world)
+    res["plan_kxx"] = plan_x
+    if multi:
+        dist.barrier(group)
+    _sync(dev)
+    t0 = time.perf_counter()
+    r0, r1 = plan_x[rank]
+    K = None
+    if rank == dst:
+        K = torch.full((n, n), float("nan"), dtype=dtype, device=dev)
+        _, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), out=K[r0:r1], dtype=dtype)
+    else:
+        strip, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), device=dev,
+                                  dtype=dtype)
+    _sync(dev)
+    t_kxx = time.perf_counter() - t0
+    if dev.type == "cuda":
+        res["peak_bytes_kxx_build"] = int(torch.cuda.max_memory_allocated(dev))
+        torch.cuda.reset_peak_memory_stats(dev)
+    el = torch.tensor([t_kxx], dtype=torch.float64)
+    if multi:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
+    res["kxx_s"] = round(float(el), 3)
+    res["kxx_s_rank"] = round(t_kxx, 3)
+    res["kxx_pairs_rank"] = px
+    say(f"  Kxx strips built in {float(el):.1f} s")
+
+    # 2. strips to dst
+    t1 = time.perf_counter()
+    if multi:
+        K = gather_strips(K if rank == dst else strip, plan_x, n, full=K, group=group, dst=dst)
+        strip = None
+    _sync(dev)
+    res["gather_kxx_s"] = round(time.perf_counter() - t1, 3)
+
+    # 3. solve on dst, Kxz strips everywhere (dst's share sized to end with the others)
+    rate = strip_cost(n, None, (0, n)) / world / max(float(el), 1e-9)
+    w = kxz_share if kxz_share is not None else kxz_weights(world, n, m, rate, solve_tflops,
+                                                            dst)
+    plan_z = strip_plan(m, n, world, weights=w)
+    res["plan_kxz"] = plan_z
+    z0, z1 = plan_z[rank]
+    alpha = None
+    t2 = time.perf_counter()
+    if rank == dst:
+        Kd = K if K.dtype == out_dtype else conv(K)
+        del K
+        alpha = solve(Kd, Y.to(dev, out_dtype))
+        _sync(dev)
+        res["solve_s"] = round(time.perf_counter() - t2, 3)
+        say(f"  solve {res['solve_s']:.2f} s")
+        res["K"] = Kd
+    t3 = time.perf_counter()
+    Kz_full = None
+    if gather_kxz and rank == dst:
+        Kz_full = torch.full((m, n), float("nan"), dtype=dtype, device=dev)
+        Kz, _, pz = gram_strip(kern, Z, X, batch_size, (z0, z1), out=Kz_full[z0:z1],
+                               dtype=dtype)
+    else:
+        Kz, _, pz = gram_strip(kern, Z, X, batch_size, (z0, z1), device=dev, dtype=dtype)
+    _sync(dev)
+    res["kxz_s_rank"] = round(time.perf_counter() - t3, 3)
+    res["kxz_pairs_rank"] = pz
+    done = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+
+    # 4. α to every rank, local scores, scores to dst
+    ncls = Y.shape[1] if Y.dim() > 1 else 1
+    if multi:
+        if rank != dst:
+            alpha = torch.empty((n, ncls), dtype=out_dtype, device=dev)
+        alpha = _bcast(alpha.reshape(n, ncls).contiguous(), dst, group)
+    alpha = alpha.reshape(n, ncls)
+    t4 = time.perf_counter()
+    sc = scores(Kz if Kz.dtype == out_dtype else conv(Kz), alpha) if z1 > z0 else \
+        torch.empty((0, ncls), dtype=out_dtype, device=dev)
+    full_sc = None
+    if rank == dst:
+        full_sc = torch.empty((m, ncls), dtype=out_dtype, device=dev)
+        full_sc[z0:z1].copy_(sc)
+    if multi:
+        full_sc = gather_strips(sc if rank != dst else None, plan_z, ncls, full=full_sc,
+                                group=group, dst=dst)
+        if gather_kxz:
+            Kz_full = gather_strips(Kz if rank != dst else None, plan_z, n, full=Kz_full,
+                                    group=group, dst=dst)
+    elif gather_kxz:
+        Kz_full = Kz
+    _sync(dev)
+    res["predict_s"] = round(time.perf_counter() - t4, 3)
+    if multi:
+        dist.all_reduce(done, op=dist.ReduceOp.MAX, group=group)
+    res["kxx_to_kxz_s"] = round(float(done), 3)
+    res["total_s"] = round(time.perf_counter() - t0, 3)
+    if rank != dst:
+        return None
+    res.update(alpha=alpha, scores=full_sc, pred=full_sc.argmax(1), Kxz=Kz_full,
+               kxz_share=w, kxz_rows=(z0, z1), Kxz_rows=Kz)
+    if dev.type == "cuda":
+        res["peak_bytes_after_kxx"] = int(torch.cuda.max_memory_allocated(dev))
+    return res

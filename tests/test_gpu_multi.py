@@ -181,3 +181,80 @@ def test_save_K_with_device_kern_matches_reference_files(n_workers):
     save_K(f, kern, "Kx_diag", dsx, None, True, 16, print_interval=1e9)
     np.testing.assert_allclose(f.d["Kx_diag"].a, z["Kx_diag"], rtol=1e-6, atol=0)
     assert f.d["Kx_diag"].chunks == tuple(z["Kx_diag_chunks"])
+
+
+def _pipeline_rank(rank, world, port, q):
+    """cnn_gp.pipeline.classify_distributed with the HIP model, rocSOLVER and the device
+    score product: world 1 in-process (rank None) or one gloo rank of a world"""
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [PKG, ROOT]
+    import torch.distributed as dist
+    import cnn_gp
+    from cnn_gp import gram
+    from cnn_gp.pipeline import classify_distributed
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        m = configs_util.model("mnist_as_tf").to("cuda", torch.float64)
+        X = _images(200, 5).cuda()
+        Z = _images(70, 6).cuda()
+        g = torch.Generator().manual_seed(7)
+        Y = cnn_gp.one_hot_pm1(torch.randint(0, 10, (200,), generator=g), 10)
+
+        def solve(K, Yd):
+            return cnn_gp.solve_system(K, Yd, jitter=1e-6, overwrite_a=True)
+
+        def scores(Kz, A):
+            return Kz @ A                  # the test's own product (same on every rank)
+
+        with torch.no_grad():
+            res = classify_distributed(gram.model_kern(m), X, Z, Y, solve, scores,
+                                       batch_size=48, gather_kxz=True)
+        out = None
+        if (rank or 0) == 0:
+            out = {k: res[k].cpu() for k in ("alpha", "pred", "scores", "Kxz")}
+            out["peak_after_kxx"] = res["peak_bytes_after_kxx"]
+            out["plan_kxx"] = res["plan_kxx"]
+        if world > 1:
+            dist.barrier()
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+    if q is None:
+        return out
+    if rank == 0:
+        q.put(out)
+
+
+def test_world2_pipeline_on_device_matches_single_process():
+    """Row strips of Kxx gathered point-to-point, solve on rank 0 while rank 1 builds its
+    Kxz rows, α broadcast, scores gathered: α and the predicted labels bit-equal to the
+    one-process run, Kxz (gathered on request) bit-equal too"""
+    single = _pipeline_rank(None, 1, None, None)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    assert len(res["plan_kxx"]) == 2
+    assert torch.equal(res["alpha"], single["alpha"])
+    assert torch.equal(res["pred"], single["pred"])
+    assert torch.equal(res["Kxz"], single["Kxz"])
+    torch.testing.assert_close(res["scores"], single["scores"], rtol=1e-12, atol=1e-12)
+    print(f"rank-0 device peak after the Kxx build: {res['peak_after_kxx'] / 1e6:.1f} MB "
+          f"(Kxx {200 * 200 * 8 / 1e6:.2f} MB)")

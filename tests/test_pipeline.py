@@ -1,0 +1,154 @@
+"""The row-strip pipeline (cnn_gp.pipeline.classify_distributed, cnn_gp.gram strips) on
+CPU: gloo ranks at world size 2 and 3 against the same function in one process, with the
+oracle as ``kern`` and scipy's posv (oracle.solve_upper, classify_gp.py:24-26) as the
+solve — test infrastructure standing in for the device model and rocSOLVER (the GPU
+variant is tests/test_gpu_multi.py).  Reference: exp_mnist_resnet/run.bash:28-43,
+classify_gp.py:39-42, 67-77; cnn_gp/data.py:11-19 (the worker split it replaces)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import nngp_oracle as O
+from oracle import specs
+
+N, M, B = 37, 13, 8
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data():
+    rng = np.random.default_rng(4)
+    X = torch.from_numpy(rng.random((N, 1, 28, 28)))
+    Z = torch.from_numpy(rng.random((M, 1, 28, 28)))
+    labels = torch.from_numpy(rng.integers(0, 10, N))
+    Y = -torch.ones((N, 10), dtype=torch.float64)
+    Y[torch.arange(N), labels] = 1.0
+    return X, Z, Y
+
+
+def _fns():
+    spec = specs.mnist_paper_convnet_gp()
+
+    def kern(x, x2, same):
+        return torch.from_numpy(O.kernel(spec, x.numpy(), x2.numpy(), same, False))
+
+    def solve(K, Y):
+        return torch.from_numpy(O.solve_upper(K.numpy(), Y.numpy(), 1e-6))
+
+    def scores(Kz, A):
+        return Kz @ A
+
+    return kern, solve, scores
+
+
+def _run(world, rank, port, q, gather):
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [PKG, ROOT]
+    from cnn_gp.pipeline import classify_distributed
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X, Z, Y = _data()
+        kern, solve, scores = _fns()
+        res = classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B, device="cpu",
+                                   gather_kxz=gather)
+        if rank == 0:
+            out = {k: res[k] for k in ("alpha", "scores", "pred", "K", "plan_kxx",
+                                       "plan_kxz")}
+            out["Kxz"] = res["Kxz"]
+            if q is None:
+                return out
+            q.put(out)
+        else:
+            assert res is None
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,gather", [(2, True), (3, False), (3, True)])
+def test_gloo_pipeline_matches_single_process(world, gather):
+    single = _run(1, 0, None, None, True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(world, r, port, q, gather)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(res["plan_kxx"]) == world
+    iu = np.triu_indices(N)
+    # every upper-triangle entry (what the solve reads) bit-equal; alpha therefore too
+    assert np.array_equal(res["K"].numpy()[iu], single["K"].numpy()[iu])
+    assert torch.equal(res["alpha"], single["alpha"])
+    assert torch.equal(res["pred"], single["pred"])
+    np.testing.assert_allclose(res["scores"].numpy(), single["scores"].numpy(), rtol=1e-12,
+                               atol=1e-12)
+    if gather:
+        assert torch.equal(res["Kxz"], single["Kxz"])
+    else:
+        assert res["Kxz"] is None
+    # against the oracle end to end: Kxx, the posv solve, argmax(Kxz @ A)
+    spec = specs.mnist_paper_convnet_gp()
+    Kref = O.kernel(spec, _data()[0].numpy())
+    np.testing.assert_allclose(res["K"].numpy()[iu], Kref[iu], rtol=1e-12)
+    X, Z, Y = _data()
+    A = O.solve_upper(Kref, Y.numpy(), 1e-6)
+    Sref = O.kernel(spec, Z.numpy(), X.numpy(), False, False) @ A
+    np.testing.assert_allclose(res["scores"].numpy(), Sref, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,n2,world", [(60000, None, 8), (10000, 60000, 8), (50000, None, 8),
+                                        (60000, None, 2), (4096, None, 3), (37, None, 3),
+                                        (13, 37, 3), (5, None, 8), (1, None, 2)])
+def test_strip_plan_partitions_and_balances(n, n2, world):
+    """contiguous strips cover [0, n); the strips' tiles cover the evaluated entries
+    exactly once; at the full-scale sizes the per-rank evaluated pairs stay within 2%"""
+    from cnn_gp.gram import strip_cost, strip_plan, strip_tiles, tile_cost, tile_plan
+    plan = strip_plan(n, n2, world)
+    assert plan[0][0] == 0 and plan[-1][1] == n
+    assert all(a[1] == b[0] and a[0] <= a[1] for a, b in zip(plan, plan[1:]))
+    costs = [strip_cost(n, n2, r) for r in plan]
+    assert sum(costs) == strip_cost(n, n2, (0, n))
+    for r in plan:
+        assert sum(tile_cost(t) for t in strip_tiles(n, n2, r, 4096)) == strip_cost(n, n2, r)
+    if n >= 10000:
+        assert max(costs) / min(costs) - 1 <= 0.02, costs
+    if n <= 64:                               # exact coverage, entry by entry
+        cov = np.zeros((n, n if n2 is None else n2), int)
+        for r in plan:
+            for same, i0, j0, a, b in strip_tiles(n, n2, r, 4):
+                blk = cov[i0:i0 + a, j0:j0 + b]
+                if same:
+                    blk[np.triu_indices(a, 1)] += 1
+                    blk[np.diag_indices(a)] += 1
+                else:
+                    blk += 1
+        want = np.triu(np.ones_like(cov)) if n2 is None else np.ones_like(cov)
+        assert np.array_equal(cov, want)
+    # one strip over the whole matrix is the reference's tile list
+    assert strip_tiles(n, n2, (0, n), 4096) == tile_plan(n, n2, 4096, 0, 1)
+
+
+def test_kxz_weights_give_the_solving_rank_less():
+    from cnn_gp.pipeline import kxz_weights
+    assert kxz_weights(1, 60000, 10000, 4e7) is None
+    w = kxz_weights(8, 60000, 10000, 4e7, solve_tflops=30)   # solve 2.4 s > 1/7 of 15 s
+    assert w[0] == 0.0 and abs(sum(w) - 1) < 1e-12
+    w = kxz_weights(2, 60000, 10000, 4e7, solve_tflops=30)
+    assert 0 < w[0] < w[1]

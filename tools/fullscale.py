@@ -4,18 +4,22 @@ exp_mnist_resnet/run.bash (save_kernel.py → merge_h5_files.py → classify_gp.
 device, in memory.
 
     python tools/fullscale.py [--n 60000 --m 10000 --tile 4096 --config mnist_as_tf]
-    torchrun --nproc-per-node 8 tools/fullscale.py ...   # tiles split, one gather to rank 0
+    torchrun --nproc-per-node 8 tools/fullscale.py ...   # row strips, gathered to rank 0
 
 bench.py runs the same function as its full-scale leg (on every rank at --gpus N).
 
 Data: synthetic MNIST-like images (values k/255, ~60% zero pixels, 4-pixel zero border;
 no dataset files here) with synthetic labels, so the accuracy line only proves the path
-runs.  Kxx keeps the reference's layout (upper tiles, NaN strictly-lower tiles) and is
-factored in place by rocSOLVER dpotrf_64 (upper triangle, like scipy's posv).
+runs.  The pipeline is cnn_gp.pipeline.classify_distributed: Kxx row strips (upper
+triangle filled; strictly-lower entries NaN or mirrored — only the upper triangle is
+read), received into the full matrix on rank 0, factored in place by rocSOLVER dpotrf_64
+(upper triangle, like scipy's posv) while the other ranks build their Kxz rows; α is
+broadcast and the [m, 10] scores gathered (Kxz itself only with --pred-var).
 
-Checks printed at the end: potrf info (positive definite), a spot check of random Kxx
-and Kxz entries recomputed one pair at a time through model(x_i, x_j, False, False), and
-the solve residual ‖Kxx·α − Y‖ / ‖Y‖ on a random subset of rows.
+Checks printed at the end: potrf info (positive definite), a HIP-vs-HIP spot check of
+random Kxx and Kxz entries recomputed one pair at a time through model(x_i, x_j, False,
+False) (oracle parity at this geometry: tests/test_gpu_fullgeom.py), and the solve
+residual ‖Kxx·α − Y‖ / ‖Y‖ on a random subset of rows.
 """
 import argparse
 import importlib
@@ -31,7 +35,6 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import cnn_gp  # noqa: E402
-from cnn_gp.gram import gather_gram, tile_cost, tile_plan  # noqa: E402
 
 
 def mnist_like(n, C, side, seed):
@@ -50,48 +53,9 @@ def log(rank, msg):
         print(msg, flush=True)
 
 
-def build(model, X, X2, B, rank, world, name, t_start, dev, out=None, dtype=torch.float64):
-    """This rank's tiles of Kxx (X2 None) or Kxz.  One rank: written straight into the
-    NaN-filled device matrix ``out``.  Several ranks: packed into one flat device buffer
-    (gram.gram_local's layout, split by evaluated pairs) for gather_gram.  Returns
-    (out or buffer, pairs evaluated)."""
-    n = len(X)
-    n2 = None if X2 is None else len(X2)
-    split = "reference" if world == 1 else "balanced"
-    tiles = tile_plan(n, n2, B, rank, world, split)
-    if world > 1:
-        cap = max(sum(a * b for *_, a, b in tile_plan(n, n2, B, r, world, split))
-                  for r in range(world))
-        out = torch.empty(max(cap, 1), dtype=dtype, device=dev)
-    pairs = 0
-    off = 0
-    last = time.perf_counter()
-    with torch.no_grad():
-        for k, (same, i0, j0, a, b) in enumerate(tiles):
-            x = X[i0:i0 + a]
-            if same:
-                t = model(x)
-            else:
-                src = X if X2 is None else X2
-                t = model(x, src[j0:j0 + b], False, False)
-            if world > 1:
-                out[off:off + a * b].view(a, b).copy_(t)
-                off += a * b
-            else:
-                out[i0:i0 + a, j0:j0 + b].copy_(t)
-            pairs += tile_cost((same, i0, j0, a, b))
-            now = time.perf_counter()
-            if now - last > 20:
-                torch.cuda.synchronize()
-                log(rank, f"  {name}: tile {k + 1}/{len(tiles)} "
-                          f"({time.perf_counter() - t_start:.0f} s)")
-                last = now
-    return out, pairs
-
-
 def widen(t):
     """float32 device matrix -> float64 (classify_gp.py:45-48's load_kern widening, on the
-    device through cgp_cast_f32_f64); the float32 source is released."""
+    device through cgp_cast_f32_f64)."""
     out = torch.empty(t.shape, dtype=torch.float64, device=t.device)
     from cnn_gp import _native as N
     N.call("cgp_cast_f32_f64", N.ptr(t), N.ptr(out), t.numel(),
@@ -102,14 +66,18 @@ def widen(t):
 def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spot=16,
               pred_var=False, rank=0, world=1, dev=None, group=None,
               kernel_dtype=torch.float64):
-    """Kxx (n) + Kxz (m × n) + rocSOLVER solve + predict on the device; with world > 1
-    the tiles are split over the ranks and gathered once to rank 0 (one RCCL gather per
-    matrix), which solves.  Returns the result dict on rank 0, None elsewhere.
+    """Kxx (n) + rocSOLVER solve + Kxz (m × n) + predict on the device, through
+    cnn_gp.pipeline.classify_distributed: with world > 1 every rank builds a row strip of
+    Kxx (balanced by evaluated pairs), rank 0 receives the strips into the full matrix and
+    solves while the other ranks build their Kxz rows, then α is broadcast and only the
+    [m, 10] scores come back.  Returns the result dict on rank 0, None elsewhere.
 
     kernel_dtype float32 runs the kernels the way the reference's own pipeline does
     (save_kernel.py:19-24: the float32 model on float32 images, K stored float32 by
     kernel_save_tools.py:21) and widens K to float64 for the solve (classify_gp.py:45-48);
     the spot check then also reports the float32 entries against the float64 model."""
+    from cnn_gp.gram import model_kern
+    from cnn_gp.pipeline import classify_distributed
     dev = dev or torch.device("cuda", torch.cuda.current_device())
     cfg = importlib.import_module(f"configs.{config}")
     model = cfg.initial_model.to(dev, kernel_dtype)
@@ -120,56 +88,79 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     g = torch.Generator().manual_seed(2)
     ytr = torch.randint(0, 10, (n,), generator=g)
     yte = torch.randint(0, 10, (m,), generator=g)
-    B = tile
-    res = {"config": config, "n": n, "m": m, "tile": B, "gpus": world,
-           "kernel_dtype": str(kernel_dtype).replace("torch.", "")}
+    Y = cnn_gp.one_hot_pm1(ytr, 10)
     kd = kernel_dtype
-
-    if world > 1:
-        dist.barrier(group)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    K = None if world > 1 else torch.full((n, n), float("nan"), dtype=kd, device=dev)
-    K, p_xx = build(model, X, None, B, rank, world, "Kxx", t0, dev, K, kd)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    Kxz = None if world > 1 else torch.full((m, n), float("nan"), dtype=kd, device=dev)
-    Kxz, p_xz = build(model, Z, X, B, rank, world, "Kxz", t0, dev, Kxz, kd)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    if world > 1:
-        # the slowest rank sets the build time; then ONE gather per matrix
-        dist.barrier(group)
-        t2 = time.perf_counter()
-        K = gather_gram(K, n, None, B, group)
-        Kxz = gather_gram(Kxz, m, n, B, group)
-        torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    res.update(kxx_s=round(t1 - t0, 2), kxz_s=round(t2 - t1, 2), gather_s=round(t3 - t2, 3),
-               kxx_pairs_per_s_rank0=round(p_xx / (t1 - t0), 1),
-               kxz_pairs_per_s_rank0=round(p_xz / max(t2 - t1, 1e-9), 1))
-    log(rank, f"kernels built in {t3 - t0:.1f} s")
-    if rank != 0:
-        if world > 1:
-            dist.barrier(group)
-        return None
-    # spot check: single pairs through the same drop-in call, other tile shapes
+    res = {"config": config, "n": n, "m": m, "tile": tile, "gpus": world,
+           "kernel_dtype": str(kd).replace("torch.", "")}
     gs = torch.Generator().manual_seed(3)
-    ii = torch.randint(0, n, (spot,), generator=gs)
-    jj = torch.randint(0, n, (spot,), generator=gs)
-    kk = torch.randint(0, m, (spot,), generator=gs)
+    rows = torch.randint(0, n, (8,), generator=gs)
+    saved = {}
+
+    def solve(K, Yd):
+        # the residual rows of K before it is factored in place (K is symmetric, its
+        # upper triangle is filled)
+        r = rows.to(K.device)
+        saved["Krows"] = torch.where(torch.arange(n, device=K.device)[None, :] >= r[:, None],
+                                     K[r], K[:, r].T)
+        return cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+
+    def scores(Kz, A):
+        out = torch.empty((Kz.shape[0], A.shape[1]), dtype=torch.float64, device=Kz.device)
+        from cnn_gp import _native as N
+        N.call("cgp_gemm_f64", N.ptr(Kz), N.ptr(A), N.ptr(out), Kz.shape[0], A.shape[1],
+               Kz.shape[1], torch.cuda.current_stream(Kz.device).cuda_stream)
+        return out
+
+    torch.cuda.reset_peak_memory_stats(dev)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        out = classify_distributed(model_kern(model), X, Z, Y, solve, scores,
+                                   batch_size=tile, group=group, device=dev, dtype=kd,
+                                   gather_kxz=pred_var,
+                                   widen=widen if kd != torch.float64 else None,
+                                   log=lambda msg: log(rank, msg))
+    wall = time.perf_counter() - t0
+    if rank != 0:
+        return None
+    kxx_bytes = n * n * 8
+    res.update({k: out[k] for k in ("kxx_s", "gather_kxx_s", "kxx_to_kxz_s", "predict_s",
+                                    "total_s")})
+    res.update(solve_s=out["solve_s"], kxz_s_rank0=out["kxz_s_rank"],
+               solve_tflops=round(n ** 3 / 3 / out["solve_s"] / 1e12, 2),
+               kxx_pairs_per_s=round(n * (n - 1) / 2 / out["kxx_s"], 1),
+               plan_kxx=out["plan_kxx"], plan_kxz=out["plan_kxz"],
+               kxz_share=out["kxz_share"],
+               rank0_peak_gb_kxx_build=round(out["peak_bytes_kxx_build"] / 1e9, 2),
+               rank0_peak_gb_after_kxx=round(out["peak_bytes_after_kxx"] / 1e9, 2),
+               rank0_peak_after_kxx_over_kxx_f64=round(out["peak_bytes_after_kxx"] /
+                                                       kxx_bytes, 3))
+    if world == 1:
+        res["kxz_s"] = out["kxz_s_rank"]
+    K, A = out["K"], out["alpha"]
+    # residual on 8 rows of the (jittered) system: ‖K·α − Y‖ / ‖Y‖
+    Kr = saved["Krows"].double()
+    Yd = Y.to(dev)
+    Kr[torch.arange(len(rows), device=dev), rows.to(dev)] += jitter
+    res["residual"] = float((Kr @ A - Yd[rows.to(dev)]).norm() / Yd[rows.to(dev)].norm())
+    res["synthetic_accuracy"] = cnn_gp.accuracy(out["pred"], yte)
+    # spot check (HIP against HIP): single pairs through the same drop-in call — other tile
+    # shapes, no chunking; a self-consistency check.  Parity with the CPU oracle at this
+    # tile geometry is tests/test_gpu_fullgeom.py.  K is factored now: Kxx entries are
+    # checked through the saved rows, Kxz entries through rank 0's own Kxz rows.
+    z0, z1 = out["kxz_rows"]
     worst = 0.0
     with torch.no_grad():
-        for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
-            a, b = min(a, b), max(a, b)
-            ref = model(X[a:a + 1], X[b:b + 1], False, False).item() if a != b else \
-                model(X[a:a + 1]).item()
-            worst = max(worst, abs(K[a, b].item() - ref) / abs(ref))
-            ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
-            worst = max(worst, abs(Kxz[c, b].item() - ref) / abs(ref))
-    # HIP against HIP: the same drop-in call on single pairs (other tile shapes, no
-    # chunking) — a self-consistency check; parity with the CPU oracle at this tile
-    # geometry is tests/test_gpu_fullgeom.py
+        for k, a in enumerate(rows.tolist()):
+            for b in torch.randint(0, n, (max(1, spot // 8),), generator=gs).tolist():
+                ref = model(X[a:a + 1]).item() if a == b else \
+                    model(X[a:a + 1], X[b:b + 1], False, False).item()
+                worst = max(worst, abs(saved["Krows"][k, b].item() - ref) / abs(ref))
+        if z1 > z0:
+            Kz = out["Kxz_rows"]
+            for c, b in zip(torch.randint(z0, z1, (spot,), generator=gs).tolist(),
+                            torch.randint(0, n, (spot,), generator=gs).tolist()):
+                ref = model(Z[c:c + 1], X[b:b + 1], False, False).item()
+                worst = max(worst, abs(Kz[c - z0, b].item() - ref) / abs(ref))
     res["spot_check_hip_vs_hip_max_rel_err"] = worst
     if kd != torch.float64:
         # the float32 entries against the float64 model on the same (exactly widened)
@@ -177,47 +168,19 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
         m64 = cfg.initial_model.to(dev, torch.float64)
         dev64 = 0.0
         with torch.no_grad():
-            for a, b, c in zip(ii.tolist(), jj.tolist(), kk.tolist()):
-                a, b = min(a, b), max(a, b)
-                xa, xb = X[a:a + 1].double(), X[b:b + 1].double()
-                ref = m64(xa, xb, False, False).item() if a != b else m64(xa).item()
-                dev64 = max(dev64, abs(K[a, b].item() - ref) / abs(ref))
-                ref = m64(Z[c:c + 1].double(), xb, False, False).item()
-                dev64 = max(dev64, abs(Kxz[c, b].item() - ref) / abs(ref))
+            for k, a in enumerate(rows.tolist()):
+                for b in (0, n // 2, n - 1):
+                    xa, xb = X[a:a + 1].double(), X[b:b + 1].double()
+                    ref = m64(xa).item() if a == b else m64(xa, xb, False, False).item()
+                    dev64 = max(dev64, abs(saved["Krows"][k, b].item() - ref) / abs(ref))
         res["spot_vs_f64_max_rel_err"] = dev64
-        torch.cuda.synchronize()
-        tw = time.perf_counter()
-        K = widen(K)                    # the solve runs in float64 (classify_gp.py:19-22)
-        Kxz = widen(Kxz)
-        torch.cuda.synchronize()
-        res["widen_s"] = round(time.perf_counter() - tw, 3)
-    # residual rows: K is symmetric, its upper triangle is filled
-    rows = torch.randint(0, n, (8,), generator=gs).to(dev)
-    Krows = torch.where(torch.arange(n, device=dev)[None, :] >= rows[:, None],
-                        K[rows], K[:, rows].T)
-    Y = cnn_gp.one_hot_pm1(ytr, 10).to(dev)
-    torch.cuda.synchronize()
-    t4 = time.perf_counter()
-    A = cnn_gp.solve_system(K, Y, jitter=jitter, overwrite_a=True)   # K -> factor
-    torch.cuda.synchronize()
-    t5 = time.perf_counter()
-    diag_j = torch.arange(len(rows), device=dev)
-    Krows[diag_j, rows] += jitter
-    r = (Krows @ A - Y[rows]).norm() / Y[rows].norm()
-    pred = cnn_gp.predict(A, Kxz)
-    torch.cuda.synchronize()
-    t6 = time.perf_counter()
-    acc = cnn_gp.accuracy(pred, yte)
-    res.update(solve_s=round(t5 - t4, 2),
-               solve_tflops=round(n ** 3 / 3 / (t5 - t4) / 1e12, 2),
-               predict_s=round(t6 - t5, 3), residual=float(r),
-               synthetic_accuracy=acc, total_s=round(t6 - t0, 2))
     if pred_var:
         with torch.no_grad():
             t7 = time.perf_counter()
             kz = model(Z, Z, True, True).double()    # Kt_diag, save_kernel.py:33-36
             torch.cuda.synchronize()
             t8 = time.perf_counter()
+            Kxz = out["Kxz"] if out["Kxz"].dtype == torch.float64 else widen(out["Kxz"])
             var = cnn_gp.predictive_variance(K, Kxz, kz, overwrite_kxz=True)
             torch.cuda.synchronize()
             t9 = time.perf_counter()
@@ -225,9 +188,8 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                    pred_var_tflops=round(n ** 2 * m / (t9 - t8) / 1e12, 2),
                    pred_var_min=float(var.min()),
                    pred_var_max_over_prior=float((var / kz).max()))
-    del K, Kxz
-    if world > 1:
-        dist.barrier(group)
+    res["wall_s"] = round(wall, 2)
+    del K, out
     return res
 
 
