@@ -21,8 +21,10 @@ Also on the same JSON line:
   mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
   solve              rocSOLVER dpotrf_64 + dpotrs_64 on the assembled 4096² Kxx
   fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
-                     + solve + predict, row-sharded over the ranks with one RCCL gather
-                     per matrix to rank 0 (tools/fullscale.py)
+                     + solve + predict, row strips per rank, Kxx received into rank 0's
+                     matrix point-to-point, solve overlapped with the Kxz strips, only
+                     the scores gathered (tools/fullscale.py, cnn_gp/pipeline.py)
+  fullscale_cifar10  BASELINE configs[4]: cifar10 Kxx 50 000² + Kxz + solve + predict
   conv_stencil_roofline  Conv2d.propagate alone (the north star's "Conv2d covariance
                      kernel") against the 8 TB/s HBM roof, PMC traffic committed
   cpu_baseline       the torch-CPU restatement of the reference (oracle/torch_cpu.py,
@@ -32,8 +34,8 @@ Also on the same JSON line:
 Multi-GPU (one process per GPU, torchrun): the Kxx grows with the world
 (n_blocks² half-tile units >= world × the 1-GPU units, divisible by world) and its tiles
 are split over the ranks by evaluated pairs — no data-path collective; per-rank work is
-~constant ("scaling": "weak").  The full-scale leg shards its fixed problem ("strong")
-and gathers once per matrix.
+~constant ("scaling": "weak").  The full-scale legs shard their fixed problems
+("strong"): Kxx strips to rank 0 point-to-point, α broadcast, scores gathered.
 """
 from __future__ import annotations
 
@@ -60,6 +62,14 @@ SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
 CLOCK_HZ = 2.4e9               # peak engine clock
 PMC_FILE = os.path.join(ROOT, "profiles", "r2", "net_pmc.json")
 CALIB_FILE = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
+PIPELINE_NOTE = (
+    "cnn_gp.pipeline.classify_distributed: Kxx row strips (B=4096 tiles) balanced by "
+    "evaluated pairs, received point-to-point into the full matrix on rank 0 (RCCL with "
+    "nccl); rank 0 factors it (blocked dpotrf/dtrsm/dsyrk, nb 2048) while the other ranks "
+    "build their Kxz row strips (rank 0's share sized to end with them); alpha broadcast, "
+    "scores = Kxz rows @ alpha per rank, only the scores gathered; solver code objects "
+    "loaded on a side thread during the Kxx build; spot check = HIP vs HIP single pairs "
+    "(oracle parity at this geometry: tests/test_gpu_fullgeom.py)")
 
 
 def parse():
@@ -537,10 +547,7 @@ def main():
         if rank == 0:
             fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
             fs["data"] = "synthetic MNIST-like (k/255, 60% zeros, 4-px zero border)"
-            fs["note"] = ("Kxx + Kxz tiles (B=4096) split over the ranks by evaluated "
-                          "pairs, one gather per matrix to rank 0 (RCCL with nccl), "
-                          "rocSOLVER solve + predict on rank 0; spot check = single pairs "
-                          "re-evaluated through model(x_i, x_j)")
+            fs["note"] = PIPELINE_NOTE
             extra["fullscale"] = fs
         torch.cuda.empty_cache()
         if not args.no_fullscale_f32:
@@ -568,9 +575,8 @@ def main():
         if rank == 0:
             fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
             fs["data"] = "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)"
-            fs["note"] = ("BASELINE configs[4] (configs/cifar10.py:4-47 architecture): Kxx + "
-                          "Kxz 10 000 x N tiles (B=4096) split over the ranks, gathered to "
-                          "rank 0, rocSOLVER solve + predict there")
+            fs["note"] = ("BASELINE configs[4] (configs/cifar10.py:4-47 architecture). " +
+                          PIPELINE_NOTE)
             extra["fullscale_cifar10"] = fs
         torch.cuda.empty_cache()
 

@@ -60,6 +60,14 @@ def _bcast(t: torch.Tensor, src: int, group):
     return t
 
 
+def _max_over_ranks(v: float, dev, group) -> float:
+    """max of a host scalar over the group (RCCL reduces device tensors only)"""
+    on = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t)
+
+
 def _sync(dev):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -69,7 +77,8 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          scores: Callable, batch_size: int = 4096, group=None, dst: int = 0,
                          device=None, dtype=torch.float64, out_dtype=torch.float64,
                          gather_kxz: bool = False, kxz_share=None, solve_tflops: float = 30.0,
-                         widen: Optional[Callable] = None, log: Optional[Callable] = None):
+                         widen: Optional[Callable] = None, log: Optional[Callable] = None,
+                         warm: Optional[Callable] = None):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
 
@@ -78,7 +87,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     ``dtype``: the kernel's output dtype (K is stored in it; float32 as the reference's
     save_kernel.py stores it); ``out_dtype``: the dtype solve and scores receive (float64:
     classify_gp.py:45-48 widens K) — ``widen(t)`` converts (default ``t.to(out_dtype)``;
-    it may release its input).  Returns on ``dst`` a dict with alpha, scores, pred, K (the
+    it may release its input).  ``warm()`` (optional) runs on ``dst`` before the Kxx build
+    and may return a thread to join before the solve (solve.warm_up_solver: the solver
+    libraries load while the kernels run).  Returns on ``dst`` a dict with alpha, scores, pred, K (the
     matrix solve saw), Kxz (when gather_kxz), dst's own Kxz rows (``kxz_rows``,
     ``Kxz_rows``), timings, the plans and the device memory peaks (overall, and from the
     end of the Kxx build: the gather, the solve and the Kxz phase); None on the other
@@ -101,6 +112,7 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
         dist.barrier(group)
     _sync(dev)
     t0 = time.perf_counter()
+    warming = warm() if (warm is not None and rank == dst) else None
     r0, r1 = plan_x[rank]
     K = None
     if rank == dst:
@@ -113,14 +125,12 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     t_kxx = time.perf_counter() - t0
     if dev.type == "cuda":
         res["peak_bytes_kxx_build"] = int(torch.cuda.max_memory_allocated(dev))
-        torch.cuda.reset_peak_memory_stats(dev)
-    el = torch.tensor([t_kxx], dtype=torch.float64)
-    if multi:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
-    res["kxx_s"] = round(float(el), 3)
+        torch.cuda.reset_peak_memory_stats(dev)      # next: the gather and the solve
+    el = _max_over_ranks(t_kxx, dev, group) if multi else t_kxx
+    res["kxx_s"] = round(el, 3)
     res["kxx_s_rank"] = round(t_kxx, 3)
     res["kxx_pairs_rank"] = px
-    say(f"  Kxx strips built in {float(el):.1f} s")
+    say(f"  Kxx strips built in {el:.1f} s")
 
     # 2. strips to dst
     t1 = time.perf_counter()
@@ -131,7 +141,7 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     res["gather_kxx_s"] = round(time.perf_counter() - t1, 3)
 
     # 3. solve on dst, Kxz strips everywhere (dst's share sized to end with the others)
-    rate = strip_cost(n, None, (0, n)) / world / max(float(el), 1e-9)
+    rate = strip_cost(n, None, (0, n)) / world / max(el, 1e-9)
     w = kxz_share if kxz_share is not None else kxz_weights(world, n, m, rate, solve_tflops,
                                                             dst)
     plan_z = strip_plan(m, n, world, weights=w)
@@ -140,6 +150,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     alpha = None
     t2 = time.perf_counter()
     if rank == dst:
+        if warming is not None:
+            warming.join()
+        t2 = time.perf_counter()
         Kd = K if K.dtype == out_dtype else conv(K)
         del K
         alpha = solve(Kd, Y.to(dev, out_dtype))
@@ -147,6 +160,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
         res["solve_s"] = round(time.perf_counter() - t2, 3)
         say(f"  solve {res['solve_s']:.2f} s")
         res["K"] = Kd
+    if dev.type == "cuda":
+        res["peak_bytes_gather_solve"] = int(torch.cuda.max_memory_allocated(dev))
+        torch.cuda.reset_peak_memory_stats(dev)      # next: the Kxz strips
     t3 = time.perf_counter()
     Kz_full = None
     if gather_kxz and rank == dst:
@@ -158,7 +174,7 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     _sync(dev)
     res["kxz_s_rank"] = round(time.perf_counter() - t3, 3)
     res["kxz_pairs_rank"] = pz
-    done = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    done = time.perf_counter() - t0
 
     # 4. α to every rank, local scores, scores to dst
     ncls = Y.shape[1] if Y.dim() > 1 else 1
@@ -185,13 +201,13 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     _sync(dev)
     res["predict_s"] = round(time.perf_counter() - t4, 3)
     if multi:
-        dist.all_reduce(done, op=dist.ReduceOp.MAX, group=group)
-    res["kxx_to_kxz_s"] = round(float(done), 3)
+        done = _max_over_ranks(done, dev, group)
+    res["kxx_to_kxz_s"] = round(done, 3)
     res["total_s"] = round(time.perf_counter() - t0, 3)
     if rank != dst:
         return None
     res.update(alpha=alpha, scores=full_sc, pred=full_sc.argmax(1), Kxz=Kz_full,
                kxz_share=w, kxz_rows=(z0, z1), Kxz_rows=Kz)
     if dev.type == "cuda":
-        res["peak_bytes_after_kxx"] = int(torch.cuda.max_memory_allocated(dev))
+        res["peak_bytes_kxz"] = int(torch.cuda.max_memory_allocated(dev))
     return res

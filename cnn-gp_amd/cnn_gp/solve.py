@@ -15,7 +15,7 @@ import torch
 from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
-           "accuracy", "one_hot_pm1", "predictive_variance")
+           "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver")
 
 
 def _device():
@@ -71,6 +71,33 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
         N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
     sol = sol.reshape(n) if vec else sol
     return sol.to(Y.device)
+
+
+def warm_up_solver(device=None, background: bool = True):
+    """Load rocBLAS / rocSOLVER's code objects for the blocked factorisation and the solve
+    (the first dpotrf / dtrsm / dsyrk / dpotrs calls of a process pay ~0.2-0.4 s for it) by
+    factoring a small identity (n = 2·2048 + 64: three diagonal blocks) on a stream of its
+    own.  With ``background`` it runs on a host thread and returns the thread: the pipeline
+    starts it before the Kxx build, so the loading overlaps the kernels."""
+    dev = torch.device(device) if device is not None else _device()
+
+    def run():
+        with torch.cuda.device(dev):
+            st = torch.cuda.Stream(dev)
+            with torch.cuda.stream(st):
+                n = 2 * 2048 + 64
+                K = torch.zeros((n, n), dtype=torch.float64, device=dev)
+                solve_system(K, torch.ones((n, 10), dtype=torch.float64, device=dev),
+                             jitter=1.0, overwrite_a=True)
+            st.synchronize()
+
+    if not background:
+        run()
+        return None
+    import threading
+    t = threading.Thread(target=run, name="cgp-solver-warmup", daemon=True)
+    t.start()
+    return t
 
 
 def predictive_variance(Kfactor, Kxz, kz_diag, overwrite_kxz: bool = False):

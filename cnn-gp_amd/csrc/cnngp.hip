@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "cnngp.h"
 #include "cgp_common.h"
@@ -1275,6 +1276,8 @@ struct BlasDev {
     rocblas_handle h = nullptr;
     std::mutex mu;
     int64_t* dinfo = nullptr;
+    int64_t* dinfos = nullptr;     // one info word per diagonal block (chol_blocked)
+    int64_t ninfos = 0;
 };
 std::mutex g_blas_reg_mu;
 std::map<int, BlasDev*> g_blas;
@@ -1318,6 +1321,73 @@ int blas_dev(hipStream_t s, BlasDev** out) {
         if (st_ != rocblas_status_success)                                             \
             return fail(CGP_EBLAS, "%s: %s", #call, rocblas_status_to_string(st_));    \
     } while (0)
+
+// Blocked right-looking Cholesky of the column-major LOWER triangle (= the row-major upper
+// triangle the reference's files fill), panel nb:
+//   for each diagonal block k:  A11 = L11·L11ᵀ (rocsolver dpotrf_64 on nb × nb),
+//                               A21 ← A21·L11⁻ᵀ (dtrsm), A22 ← A22 − A21·A21ᵀ (dsyrk, lower).
+// The trailing dsyrk carries ~all of the n³/3 flops at nb = 2048; rocSOLVER's own potrf
+// blocks far smaller and reached 33-35 TF at n = 60 000 on the MI355X, this form 58.9 TF
+// (0.75 of the fp64 peak; tools/solve_bench.hip, profiles/r3).  Only the lower triangle is
+// read or written, so the NaN strictly-upper part stays untouched.  Each block's potrf
+// writes its own info word; *info = the first failing leading minor (1-based), 0 if PD.
+#ifndef CGP_CHOL_NB
+#define CGP_CHOL_NB 2048
+#endif
+int64_t chol_nb() {
+    static const int64_t nb = [] {
+        const char* e = getenv("CGP_CHOL_NB");
+        const long long v = e ? atoll(e) : 0;
+        return v >= 64 ? (int64_t)v : (int64_t)CGP_CHOL_NB;
+    }();
+    return nb;
+}
+
+int chol_blocked(BlasDev* b, hipStream_t s, double* a, int64_t n, int64_t lda, int64_t nb,
+                 int64_t* info) {
+    rocblas_handle h = b->h;
+    const int64_t nblk = (n + nb - 1) / nb;
+    if (b->ninfos < nblk) {   // on the stream's device (the caller's current one may differ)
+        int dev = 0, cur = 0;
+        CGP_HIP(stream_device(s, &dev));
+        CGP_HIP(hipGetDevice(&cur));
+        CGP_HIP(hipSetDevice(dev));
+        if (b->dinfos) (void)hipFree(b->dinfos);
+        b->dinfos = nullptr;
+        b->ninfos = 0;
+        const hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dinfos), sizeof(int64_t) * nblk);
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) return fail(CGP_EHIP, "chol: info words: %s", hipGetErrorString(e));
+        b->ninfos = nblk;
+    }
+    CGP_HIP(hipMemsetAsync(b->dinfos, 0, sizeof(int64_t) * nblk, s));
+    CGP_BLAS(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
+    const double one = 1.0, mone = -1.0;
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        const int64_t k = blk * nb, kb = n - k < nb ? n - k : nb, m = n - k - kb;
+        double* a11 = a + k * lda + k;
+        CGP_BLAS(rocsolver_dpotrf_64(h, rocblas_fill_lower, kb, a11, lda, b->dinfos + blk));
+        if (m <= 0) break;
+        double* a21 = a11 + kb;
+        double* a22 = a + (k + kb) * lda + (k + kb);
+        CGP_BLAS(rocblas_dtrsm_64(h, rocblas_side_right, rocblas_fill_lower,
+                                  rocblas_operation_transpose, rocblas_diagonal_non_unit, m, kb,
+                                  &one, a11, lda, a21, lda));
+        CGP_BLAS(rocblas_dsyrk_64(h, rocblas_fill_lower, rocblas_operation_none, m, kb, &mone, a21,
+                                  lda, &one, a22, lda));
+    }
+    std::vector<int64_t> hinfo(nblk);
+    CGP_HIP(hipMemcpyAsync(hinfo.data(), b->dinfos, sizeof(int64_t) * nblk,
+                           hipMemcpyDeviceToHost, s));
+    CGP_HIP(hipStreamSynchronize(s));
+    *info = 0;
+    for (int64_t blk = 0; blk < nblk; ++blk)
+        if (hinfo[blk] > 0) {
+            *info = blk * nb + hinfo[blk];
+            break;
+        }
+    return CGP_OK;
+}
 
 }  // namespace
 
@@ -1470,10 +1540,16 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
         if (rc) return rc;
     }
     // row-major upper triangle == column-major lower triangle
-    CGP_BLAS(rocsolver_dpotrf_64(h, rocblas_fill_lower, n, k, ldk, b->dinfo));
     int64_t hinfo = -1;
-    CGP_HIP(hipMemcpyAsync(&hinfo, b->dinfo, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    CGP_HIP(hipStreamSynchronize(s));
+    const int64_t nb = chol_nb();
+    if (n > nb) {
+        rc = chol_blocked(b, s, k, n, ldk, nb, &hinfo);
+        if (rc) return rc;
+    } else {
+        CGP_BLAS(rocsolver_dpotrf_64(h, rocblas_fill_lower, n, k, ldk, b->dinfo));
+        CGP_HIP(hipMemcpyAsync(&hinfo, b->dinfo, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        CGP_HIP(hipStreamSynchronize(s));
+    }
     *info = hinfo;
     if (hinfo == 0) {
         CGP_BLAS(rocsolver_dpotrs_64(h, rocblas_fill_lower, n, nrhs, k, ldk, bt, ldb));

@@ -179,8 +179,11 @@ int cgp_transpose_f64(const double* src, int64_t rows, int64_t cols, double* dst
  * GP solve — replaces classify_gp.solve_system + diag_add (classify_gp.py:17-36):
  * scipy.linalg.solve(K, Y, assume_a='pos', lower=False) reads only the UPPER triangle
  * of the row-major K (its strictly-lower tiles are NaN in the reference's HDF5 files).
- *   K:  [n][ldk] row-major fp64; overwritten by the Cholesky factor (rocsolver_dpotrf_64
- *       on the column-major view = lower, i.e. the row-major upper triangle).
+ *   K:  [n][ldk] row-major fp64; overwritten by the Cholesky factor of the column-major
+ *       view's lower triangle (= the row-major upper triangle): for n > CGP_CHOL_NB (env,
+ *       default 2048) a blocked right-looking factorisation (rocsolver_dpotrf_64 per
+ *       diagonal block, rocblas_dtrsm_64 panel, rocblas_dsyrk_64 trailing update), else
+ *       rocsolver_dpotrf_64 on the whole matrix; then rocsolver_dpotrs_64.
  *   bt: the right-hand sides TRANSPOSED, [nrhs][ldb] row-major (= column-major n×nrhs);
  *       overwritten by the solution (transposed).
  *   jitter is added to K's diagonal first (diag_add, classify_gp.py:30-36).

@@ -570,6 +570,49 @@ def test_solve_leaves_kxx_by_default_and_factors_in_place_on_request():
     np.testing.assert_allclose(U.T @ U, A, rtol=1e-10, atol=1e-10 * np.abs(A).max())
 
 
+def _spd_nan_lower(n, seed, bad_from=None):
+    """a random SPD matrix (well conditioned: G Gᵀ/n + I), strictly-lower triangle NaN as in
+    the reference's files; with bad_from, the leading minor of order bad_from + 1 is made
+    indefinite (diagonal entry bad_from negative)"""
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((n, n // 4))
+    A = G @ G.T / n + np.eye(n)
+    if bad_from is not None:
+        A[bad_from, bad_from] = -1.0
+    K = A.copy()
+    K[np.tril_indices(n, -1)] = np.nan
+    return A, K
+
+
+@pytest.mark.parametrize("n", [2048, 2049, 4100, 6200])
+def test_solve_blocked_cholesky_matches_scipy(n):
+    """n > CGP_CHOL_NB (2048) runs the blocked factorisation (potrf per diagonal block,
+    trsm panel, syrk trailing update): ragged last blocks, NaN lower triangle, the factor
+    left in place equals scipy's Cholesky, the solution equals scipy's posv
+    (classify_gp.py:24-26)"""
+    import scipy.linalg
+    A, K = _spd_nan_lower(n, n)
+    rng = np.random.default_rng(1)
+    Y = rng.standard_normal((n, 10))
+    Kd = torch.from_numpy(K).to(DEV)
+    sol = cnn_gp.solve_system(Kd, torch.from_numpy(Y).to(DEV), jitter=0.5, overwrite_a=True)
+    ref = scipy.linalg.solve(A + 0.5 * np.eye(n), Y, assume_a="pos", lower=False)
+    np.testing.assert_allclose(sol.cpu().numpy(), ref, rtol=1e-10, atol=1e-12)
+    U = np.triu(Kd.cpu().numpy())
+    Uref = scipy.linalg.cholesky(A + 0.5 * np.eye(n), lower=False)
+    np.testing.assert_allclose(U, Uref, rtol=1e-10, atol=1e-12)
+    assert np.isnan(Kd.cpu().numpy()[np.tril_indices(n, -1)]).all()   # never written
+
+
+@pytest.mark.parametrize("bad", [5, 2047, 2048, 4000])
+def test_solve_blocked_not_pd_reports_the_failing_minor(bad):
+    A, K = _spd_nan_lower(4100, 3, bad_from=bad)
+    with pytest.raises(np.linalg.LinAlgError, match=f"order {bad + 1}\\)"):
+        cnn_gp.solve_system(torch.from_numpy(K).to(DEV), torch.ones(4100, 1,
+                                                                     dtype=torch.float64,
+                                                                     device=DEV))
+
+
 def test_predict_and_cast():
     rng = np.random.default_rng(9)
     Kxz = rng.random((50, 40))
