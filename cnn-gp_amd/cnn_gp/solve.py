@@ -15,7 +15,7 @@ import torch
 from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
-           "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver")
+           "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores")
 
 
 def _device():
@@ -160,19 +160,29 @@ def load_kern(dset, i, device=None):
     return out
 
 
-def predict(A, Kxz):
-    """argmax over classes of Kxz @ A (classify_gp.py:39-40), on the device."""
+def scores(Kxz, A):
+    """Kxz @ A, the class scores of classify_gp.py:39-40, on the device (rocBLAS dgemm
+    through cgp_gemm_f64): [m, n] @ [n, classes] -> [m, classes] float64."""
     dev = Kxz.device if Kxz.device.type == "cuda" else _device()
     with torch.cuda.device(dev):
         K = Kxz.to(dev, dtype=torch.float64).contiguous()
-        Ad = A.to(dev, dtype=torch.float64).contiguous()
+        Ad = A.to(dev, dtype=torch.float64).reshape(K.shape[1], -1).contiguous()
         m, kdim = K.shape
         ncls = Ad.shape[1]
-        scores = torch.empty((m, ncls), dtype=torch.float64, device=dev)
-        s = _stream(dev)
-        N.call("cgp_gemm_f64", N.ptr(K), N.ptr(Ad), N.ptr(scores), m, ncls, kdim, s)
-        pred = torch.empty((m,), dtype=torch.int64, device=dev)
-        N.call("cgp_argmax_rows_f64", N.ptr(scores), m, ncls, N.ptr(pred), s)
+        out = torch.empty((m, ncls), dtype=torch.float64, device=dev)
+        if m:
+            N.call("cgp_gemm_f64", N.ptr(K), N.ptr(Ad), N.ptr(out), m, ncls, kdim, _stream(dev))
+    return out
+
+
+def predict(A, Kxz):
+    """argmax over classes of Kxz @ A (classify_gp.py:39-40), on the device."""
+    sc = scores(Kxz, A)
+    m, ncls = sc.shape
+    with torch.cuda.device(sc.device):
+        pred = torch.empty((m,), dtype=torch.int64, device=sc.device)
+        if m:
+            N.call("cgp_argmax_rows_f64", N.ptr(sc), m, ncls, N.ptr(pred), _stream(sc.device))
     return pred
 
 

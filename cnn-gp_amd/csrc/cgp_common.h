@@ -179,15 +179,49 @@ constexpr PolyCoef poly_coef(bool quartered) {
 static __constant__ PolyCoef kReluPolyTabD = poly_coef(false);
 static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 
+// Range-adaptive ReLU (CGP_RELU_ADAPT, A/B option, off by default): lower-degree fits of P
+// on x in [0, kReluAdaptX0] and [0, kReluAdaptX1] at the same error bound
+// (tools/fit_relu_poly.py ADAPT), quartered like kReluPolyTabDq; relu_q_n takes one when
+// every active lane's pixels of the wave lie in its interval (a wave-uniform branch).
+#ifndef CGP_RELU_ADAPT
+#define CGP_RELU_ADAPT 0
+#endif
+template <int D>
+struct AdaptCoef {
+    double c[D + 1];
+};
+template <int D>
+constexpr AdaptCoef<D> adapt_coef(const double (&p)[D + 1]) {
+    AdaptCoef<D> t{};
+    for (int k = 0; k <= D; ++k) {
+        double v = p[k] * 0.0625;
+        for (int n = 0; n < k; ++n) v *= 0.25;
+        t.c[k] = v;
+    }
+    return t;
+}
+static __constant__ AdaptCoef<kReluAdaptDeg0> kReluAdaptTab0 = adapt_coef<kReluAdaptDeg0>(kReluAdaptP0);
+static __constant__ AdaptCoef<kReluAdaptDeg1> kReluAdaptTab1 = adapt_coef<kReluAdaptDeg1>(kReluAdaptP1);
+
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
     ConstD d, dq;
+#if CGP_RELU_ADAPT
+    ConstD a0, a1;
+#endif
 };
 __device__ __forceinline__ PolyTab poly_table() {
     ConstD p = (ConstD)kReluPolyTabD.c;
     ConstD q = (ConstD)kReluPolyTabDq.c;
     asm volatile("" : "+s"(p), "+s"(q));
+#if CGP_RELU_ADAPT
+    ConstD a0 = (ConstD)kReluAdaptTab0.c;
+    ConstD a1 = (ConstD)kReluAdaptTab1.c;
+    asm volatile("" : "+s"(a0), "+s"(a1));
+    return PolyTab{p, q, a0, a1};
+#else
     return PolyTab{p, q};
+#endif
 }
 // r·u + c with c in an SGPR pair: the VOP3 form (the compiler would copy c to VGPRs
 // for v_fmac_f64 instead)
@@ -268,6 +302,18 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 // sqrt(t) = T·r·(3 − T·r·r), and |cq|·Y = |c|/sqrt(t) = |rho|.  With x4 = 4x = 2 − 2|rho|,
 // 4·sqrt(x) = x4·h·(3 − x4·h·h), h = rsq(x4), the polynomial term is
 // sqrt(t)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/16 at x4/4, and max(c, 0)/2 = cq + |cq|.
+// R interleaved Horner chains of degree D with SGPR coefficients t[0..D]
+template <int R, int D>
+__device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], ConstD t) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) p[r] = fma_sc(t[D], u[r], t[D - 1]);
+#pragma unroll
+    for (int k = D - 2; k >= 0; --k) {
+        const double ck = t[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
+    }
+}
 template <int R, bool QIN>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
                                          const double (&v2)[R], const PolyTab& tab) {
@@ -291,14 +337,22 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         const double sq4 = m * __builtin_fma(-m, h, 3.0);
         sx[r] = (st[r] * u[r]) * sq4;
     }
+#if CGP_RELU_ADAPT
+    // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
+    // whose interval holds every active lane's pixels (u ≤ 4·kReluAdaptX)
+    double um = u[0];
 #pragma unroll
-    for (int r = 0; r < R; ++r) p[r] = fma_sc(tab.dq[kReluPolyDegD], u[r], tab.dq[kReluPolyDegD - 1]);
-#pragma unroll
-    for (int k = kReluPolyDegD - 2; k >= 0; --k) {
-        const double ck = tab.dq[k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
+    for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
+    if (__all(um <= 4.0 * kReluAdaptX0)) {
+        horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+    } else if (__all(um <= 4.0 * kReluAdaptX1)) {
+        horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+    } else {
+        horner_q<R, kReluPolyDegD>(p, u, tab.dq);
     }
+#else
+    horner_q<R, kReluPolyDegD>(p, u, tab.dq);
+#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = __builtin_fma(sx[r], p[r], c[r] + __builtin_fabs(c[r]));
 }

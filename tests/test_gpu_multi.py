@@ -208,11 +208,8 @@ def _pipeline_rank(rank, world, port, q):
         def solve(K, Yd):
             return cnn_gp.solve_system(K, Yd, jitter=1e-6, overwrite_a=True)
 
-        def scores(Kz, A):
-            return Kz @ A                  # the test's own product (same on every rank)
-
         with torch.no_grad():
-            res = classify_distributed(gram.model_kern(m), X, Z, Y, solve, scores,
+            res = classify_distributed(gram.model_kern(m), X, Z, Y, solve, cnn_gp.scores,
                                        batch_size=48, gather_kxz=True)
         out = None
         if (rank or 0) == 0:

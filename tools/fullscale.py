@@ -104,17 +104,10 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                      K[r], K[:, r].T)
         return cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
 
-    def scores(Kz, A):
-        out = torch.empty((Kz.shape[0], A.shape[1]), dtype=torch.float64, device=Kz.device)
-        from cnn_gp import _native as N
-        N.call("cgp_gemm_f64", N.ptr(Kz), N.ptr(A), N.ptr(out), Kz.shape[0], A.shape[1],
-               Kz.shape[1], torch.cuda.current_stream(Kz.device).cuda_stream)
-        return out
-
     torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     with torch.no_grad():
-        out = classify_distributed(model_kern(model), X, Z, Y, solve, scores,
+        out = classify_distributed(model_kern(model), X, Z, Y, solve, cnn_gp.scores,
                                    batch_size=tile, group=group, device=dev, dtype=kd,
                                    gather_kxz=pred_var,
                                    widen=widen if kd != torch.float64 else None,

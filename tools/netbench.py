@@ -25,9 +25,10 @@ def main():
     ap.add_argument("--configs", default="mnist_paper_convnet_gp,mnist_paper_residual_cnn_gp,"
                                          "mnist_as_tf,cifar10")
     ap.add_argument("--same", action="store_true", help="Kxx diagonal tile (i<j pairs)")
-    ap.add_argument("--data", default="rand", choices=["rand", "zeros", "half"],
-                    help="image data: uniform, all zero, or every pixel 0.5 (switching-"
-                         "activity probe: the arithmetic is the same, the toggling is not)")
+    ap.add_argument("--data", default="rand", choices=["rand", "zeros", "half", "mnist"],
+                    help="image data: uniform, all zero, every pixel 0.5 (switching-"
+                         "activity probe: the arithmetic is the same, the toggling is not), "
+                         "or MNIST-like (k/255, ~60%% zero pixels, 4-pixel zero border)")
     ap.add_argument("--per-stage", action="store_true",
                     help="also time each stage's launches (multi-pair stages)")
     args = ap.parse_args()
@@ -41,7 +42,18 @@ def main():
         g = torch.Generator().manual_seed(0)
         X = torch.rand((B, C, side, side), generator=g, dtype=dt).cuda()
         Z = X if args.same else torch.rand((B, C, side, side), generator=g, dtype=dt).cuda()
-        if args.data != "rand":
+        if args.data == "mnist":
+            def mnist_like(t):
+                t = torch.floor(t * 256) / 255
+                t[torch.rand(t.shape, generator=g, dtype=dt).to(t.device) < 0.6] = 0.0
+                t[..., :4, :] = 0.0
+                t[..., -4:, :] = 0.0
+                t[..., :, :4] = 0.0
+                t[..., :, -4:] = 0.0
+                return t
+            X = mnist_like(X)
+            Z = X if args.same else mnist_like(Z)
+        elif args.data != "rand":
             v = 0.0 if args.data == "zeros" else 0.5
             X = torch.full_like(X, v)
             Z = X if args.same else torch.full_like(Z, v)
