@@ -76,8 +76,9 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
 def warm_up_solver(device=None, background: bool = True):
     """Load rocBLAS / rocSOLVER's code objects for the blocked factorisation and the solve
     (the first dpotrf / dtrsm / dsyrk / dpotrs calls of a process pay ~0.2-0.4 s for it) by
-    factoring a small identity (n = 2·2048 + 64: three diagonal blocks) on a stream of its
-    own.  With ``background`` it runs on a host thread and returns the thread: the pipeline
+    factoring an identity of n = 6·2048 + 64 (seven diagonal blocks, trailing updates up
+    to 10 k wide: rocBLAS picks its large-size kernels there; 1.2 GB, ~20 ms) on a stream
+    of its own.  With ``background`` it runs on a host thread and returns the thread: the pipeline
     starts it before the Kxx build, so the loading overlaps the kernels."""
     dev = torch.device(device) if device is not None else _device()
 
@@ -85,7 +86,7 @@ def warm_up_solver(device=None, background: bool = True):
         with torch.cuda.device(dev):
             st = torch.cuda.Stream(dev)
             with torch.cuda.stream(st):
-                n = 2 * 2048 + 64
+                n = 6 * 2048 + 64
                 K = torch.zeros((n, n), dtype=torch.float64, device=dev)
                 solve_system(K, torch.ones((n, 10), dtype=torch.float64, device=dev),
                              jitter=1.0, overwrite_a=True)

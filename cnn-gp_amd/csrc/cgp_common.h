@@ -179,12 +179,17 @@ constexpr PolyCoef poly_coef(bool quartered) {
 static __constant__ PolyCoef kReluPolyTabD = poly_coef(false);
 static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 
-// Range-adaptive ReLU (CGP_RELU_ADAPT, A/B option, off by default): lower-degree fits of P
-// on x in [0, kReluAdaptX0] and [0, kReluAdaptX1] at the same error bound
-// (tools/fit_relu_poly.py ADAPT), quartered like kReluPolyTabDq; relu_q_n takes one when
-// every active lane's pixels of the wave lie in its interval (a wave-uniform branch).
+// Range-adaptive ReLU (CGP_RELU_ADAPT, default on): lower-degree fits of P on x in
+// [0, kReluAdaptX0/1/2] = [0, 1/8], [0, 1/4], [0, 3/8] (degrees 7, 9, 11) at the error bound
+// of the full degree-13 fit (5.8e-15 / 8.2e-15 / 8.6e-15 vs 1.6e-14; tools/fit_relu_poly.py
+// ADAPT), quartered like kReluPolyTabDq.  relu_q_n takes the shortest one whose interval
+// holds every active lane's pixels of the wave (a wave-uniform branch).  Deep layers have
+// |rho| near 1 (x small): on MNIST-like pairs the ConvNet's ReLUs 2-7 have x <= 0.24 and its
+// last four x <= 0.125.  Only one-pair code uses it (AD in relu_n): there a
+// wave holds one pair's pixels, so a pair's result never depends on the other pairs of
+// its tile; multi-pair stages keep the full polynomial.
 #ifndef CGP_RELU_ADAPT
-#define CGP_RELU_ADAPT 0
+#define CGP_RELU_ADAPT 1
 #endif
 template <int D>
 struct AdaptCoef {
@@ -202,12 +207,13 @@ constexpr AdaptCoef<D> adapt_coef(const double (&p)[D + 1]) {
 }
 static __constant__ AdaptCoef<kReluAdaptDeg0> kReluAdaptTab0 = adapt_coef<kReluAdaptDeg0>(kReluAdaptP0);
 static __constant__ AdaptCoef<kReluAdaptDeg1> kReluAdaptTab1 = adapt_coef<kReluAdaptDeg1>(kReluAdaptP1);
+static __constant__ AdaptCoef<kReluAdaptDeg2> kReluAdaptTab2 = adapt_coef<kReluAdaptDeg2>(kReluAdaptP2);
 
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
     ConstD d, dq;
 #if CGP_RELU_ADAPT
-    ConstD a0, a1;
+    ConstD a0, a1, a2;
 #endif
 };
 __device__ __forceinline__ PolyTab poly_table() {
@@ -217,8 +223,9 @@ __device__ __forceinline__ PolyTab poly_table() {
 #if CGP_RELU_ADAPT
     ConstD a0 = (ConstD)kReluAdaptTab0.c;
     ConstD a1 = (ConstD)kReluAdaptTab1.c;
-    asm volatile("" : "+s"(a0), "+s"(a1));
-    return PolyTab{p, q, a0, a1};
+    ConstD a2 = (ConstD)kReluAdaptTab2.c;
+    asm volatile("" : "+s"(a0), "+s"(a1), "+s"(a2));
+    return PolyTab{p, q, a0, a1, a2};
 #else
     return PolyTab{p, q};
 #endif
@@ -314,7 +321,7 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
         for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
 }
-template <int R, bool QIN>
+template <int R, bool QIN, bool AD = false>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
                                          const double (&v2)[R], const PolyTab& tab) {
     double y[R], st[R], sx[R], u[R], p[R];   // u: x4
@@ -338,15 +345,21 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         sx[r] = (st[r] * u[r]) * sq4;
     }
 #if CGP_RELU_ADAPT
-    // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
-    // whose interval holds every active lane's pixels (u ≤ 4·kReluAdaptX)
-    double um = u[0];
+    if constexpr (AD) {
+        // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
+        // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
+        double um = u[0];
 #pragma unroll
-    for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
-    if (__all(um <= 4.0 * kReluAdaptX0)) {
-        horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
-    } else if (__all(um <= 4.0 * kReluAdaptX1)) {
-        horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
+        if (__all(um <= 4.0 * kReluAdaptX0)) {
+            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+        } else if (__all(um <= 4.0 * kReluAdaptX1)) {
+            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        } else if (__all(um <= 4.0 * kReluAdaptX2)) {
+            horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
+        } else {
+            horner_q<R, kReluPolyDegD>(p, u, tab.dq);
+        }
     } else {
         horner_q<R, kReluPolyDegD>(p, u, tab.dq);
     }

@@ -310,15 +310,16 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
 template <typename T, bool EX>
 constexpr bool kQuarter = !EX && sizeof(T) == 8;
 
-// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4)
-template <bool EXACT, bool QIN, typename T, int R>
+// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4; AD: the caller's
+// waves hold one pair's pixels, so the fp64 form may take the range-adaptive polynomial)
+template <bool EXACT, bool QIN, typename T, int R, bool AD = false>
 __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
                                        const PolyTab& tab) {
     if constexpr (EXACT) {
 #pragma unroll
         for (int k = 0; k < R; ++k) v[k] = relu_exact_inl(v[k], u1[k], u2[k]);
     } else if constexpr (sizeof(T) == 8) {
-        relu_q_n<R, QIN>(v, u1, u2, tab);
+        relu_q_n<R, QIN, AD>(v, u1, u2, tab);
     } else {
         relu_fast_n<R>(v, u1, u2, tab);
     }
@@ -346,12 +347,12 @@ constexpr int res_index(int h, int w) {
 // relu(result) -> dst2 (the next block's ReLU branch input, saving a separate op).
 // An op has the ReLU or dst2, never both, so one set of prefetched variances (u1, u2)
 // serves either.
-template <typename T, bool EX, bool DU, int R>
+template <typename T, bool EX, bool DU, int R, bool AD = false>
 __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& op, T (&v)[R],
                                         const int (&at)[R], const bool (&ok)[R],
                                         const T (&u1)[R], const T (&u2)[R],
                                         const PolyTab& tab) {
-    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, R>(v, u1, u2, tab);
+    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, R, AD>(v, u1, u2, tab);
     if (op.add >= 0) {
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -361,7 +362,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
     for (int k = 0; k < R; ++k)
         if (ok[k]) lds[op.dst + at[k]] = v[k];
     if (DU && op.dst2 >= 0) {
-        relu_n<EX, false, T, R>(v, u1, u2, tab);
+        relu_n<EX, false, T, R, AD>(v, u1, u2, tab);
 #pragma unroll
         for (int k = 0; k < R; ++k)
             if (ok[k]) lds[op.dst2 + at[k]] = v[k];
@@ -528,7 +529,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
-        net_out<T, EX, DU, KP>(lds, op, v, at, ok, u1, u2, tab);
+        net_out<T, EX, DU, KP, NP == 1>(lds, op, v, at, ok, u1, u2, tab);
     } else if constexpr (G::DIRECT) {
         // one pass: item (q, g3, c) sums its WIN3 x TAPS input window straight from the
         // source slot (row sums, then column sums: the separable path's order, so the
@@ -601,7 +602,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
-                net_out<T, EX, DU, G::R3>(lds, op, res[kv], at, ok, u1[kv], u2[kv], tab);
+                net_out<T, EX, DU, G::R3, NP == 1>(lds, op, res[kv], at, ok, u1[kv], u2[kv],
+                                                   tab);
             }
         }
     } else {
@@ -688,7 +690,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
-                net_out<T, EX, DU, G::R3>(lds, op, v, at, ok, u1[kv], u2[kv], tab);
+                net_out<T, EX, DU, G::R3, NP == 1>(lds, op, v, at, ok, u1[kv], u2[kv], tab);
             }
         }
     }
@@ -766,7 +768,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         }
     }
     if constexpr (KIND == CGP_NET_RELU) {
-        if (live) relu_n<EX, false, T, KE>(a, u1, u2, tab);
+        if (live) relu_n<EX, false, T, KE, NP == 1>(a, u1, u2, tab);
         if (op.add >= 0) {
 #pragma unroll
             for (int k = 0; k < KE; ++k)
@@ -778,7 +780,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         if (ok[k]) lds[op.dst + at[k]] = a[k];
     if constexpr (KIND == CGP_NET_LINEAR && DU) {
         if (op.dst2 >= 0) {
-            if (live) relu_n<EX, false, T, KE>(a, u1, u2, tab);
+            if (live) relu_n<EX, false, T, KE, NP == 1>(a, u1, u2, tab);
 #pragma unroll
             for (int k = 0; k < KE; ++k)
                 if (ok[k]) lds[op.dst2 + at[k]] = a[k];

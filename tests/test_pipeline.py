@@ -152,3 +152,18 @@ def test_kxz_weights_give_the_solving_rank_less():
     assert w[0] == 0.0 and abs(sum(w) - 1) < 1e-12
     w = kxz_weights(2, 60000, 10000, 4e7, solve_tflops=30)
     assert 0 < w[0] < w[1]
+
+
+def test_strip_plan_weights_zero_share_for_the_solving_rank():
+    """rank 0 with weight 0 (its solve outlasts a share of Kxz) gets an empty strip; the
+    other ranks split the rows evenly"""
+    from cnn_gp.gram import strip_cost, strip_plan, strip_tiles
+    w = [0.0] + [1.0] * 7
+    plan = strip_plan(10000, 60000, 8, weights=w)
+    assert plan[0] == (0, 0) and strip_tiles(10000, 60000, plan[0], 4096) == []
+    costs = [strip_cost(10000, 60000, r) for r in plan[1:]]
+    assert max(costs) / min(costs) - 1 <= 0.01 and sum(costs) == 10000 * 60000
+    # a half share
+    plan = strip_plan(10000, 60000, 3, weights=[0.5, 1, 1])
+    rows = [b - a for a, b in plan]
+    assert abs(rows[0] - 2000) <= 8 and abs(rows[1] - 4000) <= 8

@@ -6,8 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r3d
 mkdir -p $O
-/usr/bin/time -f "bench wall %e s" timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-tail -1 $O/bench.err
+T0=$SECONDS; timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }; echo "bench wall $((SECONDS - T0)) s"
+
 python -c "
 import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
 print('value', d['value'], 'tf', d['mnist_as_tf']['value'], 'roof', d['roofline']['frac'], d['roofline']['avg_ms'])
