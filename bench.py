@@ -17,7 +17,7 @@ Also on the same JSON line:
   roofline           the whole-network kernel (net_kernel, fp64 VALU-bound): credited
                      direct-stencil flops vs the fp64 peak, plus the VALU issue
                      utilisation and HBM traffic per launch from the committed PMC
-                     passes (profiles/r2/net_pmc.json, rocprofv3)
+                     passes (profiles/r3/net_pmc.json, rocprofv3)
   mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
   solve              rocSOLVER dpotrf_64 + dpotrs_64 on the assembled 4096² Kxx
   fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
@@ -60,7 +60,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
 FP64_PEAK_TFLOPS = 78.6        # MI355X spec FP64 (vector = matrix); half the FP32 157.3
 SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
 CLOCK_HZ = 2.4e9               # peak engine clock
-PMC_FILE = os.path.join(ROOT, "profiles", "r2", "net_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r3", "net_pmc.json")
 CALIB_FILE = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
 PIPELINE_NOTE = (
     "cnn_gp.pipeline.classify_distributed: Kxx row strips (B=4096 tiles) balanced by "
@@ -161,7 +161,7 @@ def conv_stencil_roofline(model, x, B, reps=5):
     the B·B pair maps of one tile, timed with HIP events on the launch stream; against the
     8 TB/s HBM roof with algorithmic bytes 8·P·(H·W + Ho·Wo).  A torch copy of the same
     input is timed beside it as the achievable-bandwidth reference.  ``traffic``: the
-    committed PMC pass over the same launch (profiles/r2/net_pmc.json "conv_stencil")."""
+    committed PMC pass over the same launch (profiles/r3/net_pmc.json "conv_stencil")."""
     from collections import Counter
     _, C, h, w = x.shape
     plan = model._plan(h, w)

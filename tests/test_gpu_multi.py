@@ -216,7 +216,7 @@ def _pipeline_rank(rank, world, port, q):
             # numpy: pickled by value (a torch tensor on an mp queue travels as a shared
             # memory handle, which dies with this process)
             out = {k: res[k].cpu().numpy() for k in ("alpha", "pred", "scores", "Kxz")}
-            out["peak_after_kxx"] = res["peak_bytes_after_kxx"]
+            out["peak_gather_solve"] = res["peak_bytes_gather_solve"]
             out["plan_kxx"] = res["plan_kxx"]
         if world > 1:
             dist.barrier()
@@ -255,5 +255,5 @@ def test_world2_pipeline_on_device_matches_single_process():
     assert np.array_equal(res["pred"], single["pred"])
     assert np.array_equal(res["Kxz"], single["Kxz"])
     np.testing.assert_allclose(res["scores"], single["scores"], rtol=1e-12, atol=1e-12)
-    print(f"rank-0 device peak after the Kxx build: {res['peak_after_kxx'] / 1e6:.1f} MB "
+    print(f"rank-0 device peak in the gather + solve: {res['peak_gather_solve'] / 1e6:.1f} MB "
           f"(Kxx {200 * 200 * 8 / 1e6:.2f} MB)")
