@@ -22,6 +22,7 @@ CGP_PRE_NONE, CGP_PRE_RELU, CGP_PRE_MOMENTS = 0, 1, 2
 CGP_POST_NONE, CGP_POST_RELU = 0, 1
 CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
 CGP_NET_LOAD, CGP_NET_STORE = 4, 5
+CGP_NET_CODE_HS_CLEAN = 0x100
 CGP_VAR_MOMENTS, CGP_VAR_CONV, CGP_VAR_HALF, CGP_VAR_SUM = 0, 1, 2, 3
 
 _vp = ctypes.c_void_p

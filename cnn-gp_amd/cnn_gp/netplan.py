@@ -92,6 +92,7 @@ class Stage:
     final: bool
     load_stride: int                   # elements per unit of the incoming state record
     store_stride: int                  # ... of the outgoing one
+    hs: int = 0                        # LDS cell of a one-pair reduction's partial sums
 
     @property
     def n_ops(self):
@@ -493,6 +494,8 @@ class NetPlan:
                     continue
                 folded.append((f, v))
             recs = folded
+        hs_part = self._reduce_cells(recs)
+        self._mark_hs_clean(recs, pairs, hs_part)
         for f, _ in recs:
             # (a two-pair stage runs its ops as one-pair halves: lowered like one pair)
             if f["kind"] == N.CGP_NET_RELU or (f["kind"] == N.CGP_NET_LINEAR and pairs > 2):
@@ -503,7 +506,65 @@ class NetPlan:
             if pairs == 1:
                 raise Unsupported(f"LDS footprint {top * itemsize} B")
         return Stage(records=recs, lds_elems=top, final_slot=final_origin, pairs=pairs,
-                     final=final, load_stride=load_stride, store_stride=store_stride)
+                     final=final, load_stride=load_stride, store_stride=store_stride,
+                     hs=hs_part)
+
+    def _hs_cells(self, f):
+        """(zero cells, data cells) a separable conv's row pass leaves in the row-sum
+        scratch (the arena's first HSR·WO cells: hs row q <-> input row q + off; rows
+        outside the input are zero rows), or None for a conv without scratch (1x1,
+        full-map reduction, single-pass <= 3 taps: cgp_net_hs_elems() <= 2)."""
+        h, w, ho, wo, taps, s, off = f["geom"]
+        hs_elems = self._lib.cgp_net_hs_elems(f["code"] & (N.CGP_NET_CODE_HS_CLEAN - 1))
+        if hs_elems <= 2:
+            return None
+        hsr = (ho - 1) * s + taps
+        q0, q1 = max(0, -off), min(hsr, h - off)
+        assert hsr * wo == hs_elems, (f["geom"], hs_elems)
+        zero = set(range(0, q0 * wo)) | set(range(q1 * wo, hsr * wo))
+        return zero, set(range(q0 * wo, q1 * wo))
+
+    def _reduce_cells(self, recs):
+        """Where a one-pair full-map reduction puts its two wave partial sums (cgp_net_args.hs):
+        inside the data rows of every separable conv's row-sum scratch, which each row pass
+        rewrites anyway — so the partials never land on a zero row; 0 without separable
+        convs."""
+        lo, hi = 0, 1 << 30
+        for f, _ in recs:
+            if f["kind"] == N.CGP_NET_CONV:
+                cells = self._hs_cells(f)
+                if cells is not None:
+                    data = cells[1]
+                    lo, hi = max(lo, min(data)), min(hi, max(data) + 1)
+        return lo if lo + 2 <= hi else 0
+
+    def _mark_hs_clean(self, recs, pairs, hs_part=0):
+        """CGP_NET_CODE_HS_CLEAN on every separable conv whose zero rows of the row-sum
+        scratch are still zero when it runs: the op list repeats for every pair a
+        workgroup walks (LDS is zeroed once at kernel start), so the walk below runs it
+        twice — the first pass from the zeroed start, the second from the steady state —
+        and a conv is clean only if no data sits on its zero rows in either.  Writers of
+        scratch cells: separable row passes (their input rows) and a one-pair full-map
+        reduction (its two wave partial sums at cells hs_part, hs_part + 1)."""
+        dirty, need = set(), set()
+        for _ in range(2):
+            for idx, (f, _) in enumerate(recs):
+                if f["kind"] != N.CGP_NET_CONV:
+                    continue
+                cells = self._hs_cells(f)
+                if cells is not None:
+                    zero, data = cells
+                    if zero & dirty:
+                        need.add(idx)
+                    dirty = (dirty - zero) | data
+                else:
+                    h, w, ho, wo, taps, s, off = f["geom"]
+                    if ho == wo == 1 and off == 0 and taps == h == w and pairs <= 2:
+                        dirty |= {hs_part, hs_part + 1}
+        for idx, (f, _) in enumerate(recs):
+            if f["kind"] == N.CGP_NET_CONV and self._hs_cells(f) is not None and \
+                    idx not in need:
+                f["code"] |= N.CGP_NET_CODE_HS_CLEAN
 
     def lds_bytes(self, itemsize: int) -> int:
         return self.lds_elems * itemsize
@@ -611,7 +672,7 @@ class NetPlan:
             a.ops = ops_dev.data_ptr()
             a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
             a.nops, a.channels, a.h, a.w = st.n_ops, x.shape[1], x.shape[2], x.shape[3]
-            a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, 0, st.lds_elems
+            a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, st.hs, st.lds_elems
             a.flags = flags | (N.CGP_FLAG_NET_DUAL if st.dual else 0)
             a.pairs = st.pairs
             a.final_stage = int(st.final)

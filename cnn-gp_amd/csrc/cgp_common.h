@@ -321,9 +321,15 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
         for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
 }
-template <int R, bool QIN, bool AD = false>
+// AD: 0 the full polynomial; 1 the range-adaptive choice, uniform over the wave (its lanes
+// hold one pair); 2 the choice per pair segment: `seg` is the mask of this wave's lanes that
+// hold the same pair as this lane (multi-pair stages, CGP_RELU_ADAPT_MP), so a pair's
+// polynomial depends on its own pixels only and a wave whose pairs disagree runs each
+// chosen polynomial under its lanes' exec mask
+template <int R, bool QIN, int AD = 0>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
-                                         const double (&v2)[R], const PolyTab& tab) {
+                                         const double (&v2)[R], const PolyTab& tab,
+                                         unsigned long long seg = ~0ull) {
     double y[R], st[R], sx[R], u[R], p[R];   // u: x4
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -345,7 +351,22 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         sx[r] = (st[r] * u[r]) * sq4;
     }
 #if CGP_RELU_ADAPT
-    if constexpr (AD) {
+    if constexpr (AD == 2) {
+        double um = u[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
+        const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
+        auto all_seg = [&](bool pred) { return (__ballot(pred) & seg) == ex; };
+        if (all_seg(um <= 4.0 * kReluAdaptX0)) {
+            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+        } else if (all_seg(um <= 4.0 * kReluAdaptX1)) {
+            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        } else if (all_seg(um <= 4.0 * kReluAdaptX2)) {
+            horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
+        } else {
+            horner_q<R, kReluPolyDegD>(p, u, tab.dq);
+        }
+    } else if constexpr (AD == 1) {
         // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
         // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
         double um = u[0];

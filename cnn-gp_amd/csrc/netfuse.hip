@@ -312,14 +312,14 @@ constexpr bool kQuarter = !EX && sizeof(T) == 8;
 
 // R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4; AD: the caller's
 // waves hold one pair's pixels, so the fp64 form may take the range-adaptive polynomial)
-template <bool EXACT, bool QIN, typename T, int R, bool AD = false>
+template <bool EXACT, bool QIN, typename T, int R, int AD = 0>
 __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
-                                       const PolyTab& tab) {
+                                       const PolyTab& tab, unsigned long long seg = ~0ull) {
     if constexpr (EXACT) {
 #pragma unroll
         for (int k = 0; k < R; ++k) v[k] = relu_exact_inl(v[k], u1[k], u2[k]);
     } else if constexpr (sizeof(T) == 8) {
-        relu_q_n<R, QIN, AD>(v, u1, u2, tab);
+        relu_q_n<R, QIN, AD>(v, u1, u2, tab, seg);
     } else {
         relu_fast_n<R>(v, u1, u2, tab);
     }
@@ -347,12 +347,12 @@ constexpr int res_index(int h, int w) {
 // relu(result) -> dst2 (the next block's ReLU branch input, saving a separate op).
 // An op has the ReLU or dst2, never both, so one set of prefetched variances (u1, u2)
 // serves either.
-template <typename T, bool EX, bool DU, int R, bool AD = false>
+template <typename T, bool EX, bool DU, int R, int AD = 0>
 __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& op, T (&v)[R],
                                         const int (&at)[R], const bool (&ok)[R],
                                         const T (&u1)[R], const T (&u2)[R],
-                                        const PolyTab& tab) {
-    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, R, AD>(v, u1, u2, tab);
+                                        const PolyTab& tab, unsigned long long seg = ~0ull) {
+    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, R, AD>(v, u1, u2, tab, seg);
     if (op.add >= 0) {
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -362,7 +362,7 @@ __device__ __forceinline__ void net_out(T* __restrict__ lds, const cgp_net_op& o
     for (int k = 0; k < R; ++k)
         if (ok[k]) lds[op.dst + at[k]] = v[k];
     if (DU && op.dst2 >= 0) {
-        relu_n<EX, false, T, R, AD>(v, u1, u2, tab);
+        relu_n<EX, false, T, R, AD>(v, u1, u2, tab, seg);
 #pragma unroll
         for (int k = 0; k < R; ++k)
             if (ok[k]) lds[op.dst2 + at[k]] = v[k];
@@ -428,6 +428,23 @@ __device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, u
 // ---- CGP_NET_CONV -------------------------------------------------------------------
 // G::NP pairs: item it of a pass belongs to pair q = it / (items per pair) and works on
 // that pair's LDS arena (q · lds_elems) and variance maps.
+// Range-adaptive ReLU in a conv epilogue: one-pair code votes over the wave (AD 1);
+// multi-pair stages vote per pair segment of the wave (AD 2) with CGP_RELU_ADAPT_MP.
+#ifndef CGP_RELU_ADAPT_MP
+#define CGP_RELU_ADAPT_MP 0
+#endif
+template <int NP>
+constexpr int kAdaptOf = NP == 1 ? 1 : (CGP_RELU_ADAPT_MP ? 2 : 0);
+// lanes of this wave whose item belongs to the same pair as item `it` (items of pair q
+// are [q·per, (q+1)·per); item it sits on lane it % 64 of its wave)
+__device__ __forceinline__ unsigned long long pair_lanes(int it, int per) {
+    const int wb = it & ~63, q = udiv(it, per);
+    int lo = q * per - wb, hi = (q + 1) * per - wb;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 64 ? 64 : hi;
+    const unsigned long long top = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+    return top & ~((1ull << lo) - 1ull);
+}
 template <typename T, bool EX, bool DU, class G>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, const Pairs& pr) {
@@ -529,7 +546,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
-        net_out<T, EX, DU, KP, NP == 1>(lds, op, v, at, ok, u1, u2, tab);
+        net_out<T, EX, DU, KP, NP == 1 ? 1 : 0>(lds, op, v, at, ok, u1, u2, tab);
     } else if constexpr (G::DIRECT) {
         // one pass: item (q, g3, c) sums its WIN3 x TAPS input window straight from the
         // source slot (row sums, then column sums: the separable path's order, so the
@@ -602,8 +619,9 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
-                net_out<T, EX, DU, G::R3, NP == 1>(lds, op, res[kv], at, ok, u1[kv], u2[kv],
-                                                   tab);
+                net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, res[kv], at, ok, u1[kv],
+                                                        u2[kv], tab,
+                                                        NP == 1 ? ~0ull : pair_lanes(it, G::NV));
             }
         }
     } else {
@@ -651,14 +669,17 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 for (int t = 0; t < G::R2; ++t) h[t] = o[t];
             }
         }
-        // hs rows outside the input are zero (the scratch is shared by every conv)
+        // hs rows outside the input are zero (the scratch is shared by every conv); skipped
+        // when the host proved they still are (CGP_NET_CODE_HS_CLEAN)
         if constexpr (G::NZ > 0) {
+            if (!(op.code & CGP_NET_CODE_HS_CLEAN)) {
 #pragma unroll
-            for (int z0 = 0; z0 < NZT; z0 += G::NT) {
-                const int z = z0 + tid;
-                if (NZT % G::NT == 0 || z < NZT) {
-                    const int q = NP == 1 ? 0 : udiv(z, G::NZ), zl = z - q * G::NZ;
-                    hs[q * arena + (zl < G::Q0 * G::WO ? zl : zl + G::NVR * G::WO)] = T(0);
+                for (int z0 = 0; z0 < NZT; z0 += G::NT) {
+                    const int z = z0 + tid;
+                    if (NZT % G::NT == 0 || z < NZT) {
+                        const int q = NP == 1 ? 0 : udiv(z, G::NZ), zl = z - q * G::NZ;
+                        hs[q * arena + (zl < G::Q0 * G::WO ? zl : zl + G::NVR * G::WO)] = T(0);
+                    }
                 }
             }
         }
@@ -690,7 +711,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
-                net_out<T, EX, DU, G::R3, NP == 1>(lds, op, v, at, ok, u1[kv], u2[kv], tab);
+                net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, v, at, ok, u1[kv], u2[kv], tab,
+                                                        NP == 1 ? ~0ull : pair_lanes(it, G::NV));
             }
         }
     }
@@ -768,7 +790,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         }
     }
     if constexpr (KIND == CGP_NET_RELU) {
-        if (live) relu_n<EX, false, T, KE, NP == 1>(a, u1, u2, tab);
+        if (live) relu_n<EX, false, T, KE, NP == 1 ? 1 : 0>(a, u1, u2, tab);
         if (op.add >= 0) {
 #pragma unroll
             for (int k = 0; k < KE; ++k)
@@ -780,7 +802,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         if (ok[k]) lds[op.dst + at[k]] = a[k];
     if constexpr (KIND == CGP_NET_LINEAR && DU) {
         if (op.dst2 >= 0) {
-            if (live) relu_n<EX, false, T, KE, NP == 1>(a, u1, u2, tab);
+            if (live) relu_n<EX, false, T, KE, NP == 1 ? 1 : 0>(a, u1, u2, tab);
 #pragma unroll
             for (int k = 0; k < KE; ++k)
                 if (ok[k]) lds[op.dst2 + at[k]] = a[k];
@@ -949,7 +971,7 @@ __device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op
     }
     switch (op.kind) {
     case CGP_NET_CONV:
-        switch (op.code) {
+        switch (op.code & (CGP_NET_CODE_HS_CLEAN - 1)) {
             CGP_NET_GEOMETRIES(CGP_NET_CASE)
         default:
             break;
@@ -1029,7 +1051,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
             }
         }
         if constexpr (o.kind == CGP_NET_CONV) {
-            constexpr GeoRow g = kGeoTable[o.code];
+            constexpr GeoRow g = kGeoTable[o.code & (CGP_NET_CODE_HS_CLEAN - 1)];
             net_conv<T, false, DU, NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>>(lds, op, p,
                                                                                     pr);
         } else if constexpr (o.kind == CGP_NET_RELU || o.kind == CGP_NET_LINEAR ||

@@ -250,11 +250,20 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
 #define CGP_NET_LINEAR 3
 #define CGP_NET_LOAD 4     /* stage input:  slot dst <- state[unit][add .. add + h·w) */
 #define CGP_NET_STORE 5    /* stage output: state[unit][add .. add + h·w) <- slot src */
+/* CONV code flag: a separable conv writes the rows of its row-sum scratch that lie outside
+ * its input as zeros before its column pass; with this flag it skips them (the host has
+ * proved no op since their last zeroing wrote there — cyclically over the stage's op
+ * list, which repeats for every pair a workgroup walks).  The scratch is the LDS arena's
+ * first cells: separable row passes write their input rows there and a one-pair
+ * full-map reduction its two wave partial sums. */
+#define CGP_NET_CODE_HS_CLEAN 0x100
 
 typedef struct cgp_net_op {
     int32_t kind;          /* CGP_NET_* */
-    int32_t code;          /* CONV: cgp_net_geometry();  RELU/LINEAR/MOMENTS:
-                              cgp_net_resolution() of the map, or -1 (generic) */
+    int32_t code;          /* CONV: cgp_net_geometry(), | CGP_NET_CODE_HS_CLEAN when the row
+                              sums' zero rows are known to be zero already;
+                              RELU/LINEAR/MOMENTS: cgp_net_resolution() of the map, or -1
+                              (generic) */
     int32_t src, dst, add; /* LDS element offsets of the slots' (0, 0) pixel; add < 0: none */
     int32_t ws_in, ws_out; /* row strides (elements) of the src slot / dst and add slots */
     int32_t relu;          /* CONV: apply the ReLU map to the conv output (then + add) */

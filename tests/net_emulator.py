@@ -15,6 +15,7 @@ import numpy as np
 from oracle import nngp_oracle as O
 
 TINY = O.F32_TINY
+HS_CLEAN = 0x100            # cgp_net_op.code flag (include/cnngp.h CGP_NET_CODE_HS_CLEAN)
 
 
 def _conv_maps(m, geom, weight, bias):
@@ -100,20 +101,44 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
         elif kind == 0:                                         # CONV
             h, w, ho, wo, taps, s, off = f["geom"]
             src = lds[plane(f["src"], h, w, f["ws_in"])]
-            # row pass over the planned slot (reads the halo columns from `lds`)
+            point = taps == 1 and off == 0
+            reduce = ho == wo == 1 and off == 0 and taps == h == w
+            separable = not point and not reduce and taps > 3
             hsr = (ho - 1) * s + taps
-            hs = np.zeros((hsr, wo))
-            for q in range(hsr):
-                r = q + off
-                if not 0 <= r < h:
-                    continue
-                for c in range(wo):
-                    base = f["src"] + r * f["ws_in"] + c * s + off
-                    hs[q, c] = lds[base:base + taps].sum()
+            if separable:
+                # the row pass writes its input rows into the arena's first cells (the
+                # kernel's row-sum scratch); rows outside the input are zero rows, rewritten
+                # unless the host marked them clean (cgp_net_op.code & HS_CLEAN) — stale
+                # data there would reach the column pass, as on the device
+                q0, q1 = max(0, -off), min(hsr, h - off)
+                for q in range(q0, q1):
+                    r = q + off
+                    for c in range(wo):
+                        base = f["src"] + r * f["ws_in"] + c * s + off
+                        lds[hs0 + q * wo + c] = lds[base:base + taps].sum()
+                if not f["code"] & HS_CLEAN:
+                    lds[hs0:hs0 + q0 * wo] = 0.0
+                    lds[hs0 + q1 * wo:hs0 + hsr * wo] = 0.0
+                hs = lds[hs0:hs0 + hsr * wo].reshape(hsr, wo).copy()
+            else:
+                # row pass over the planned slot (reads the halo columns from `lds`)
+                hs = np.zeros((hsr, wo))
+                for q in range(hsr):
+                    r = q + off
+                    if not 0 <= r < h:
+                        continue
+                    for c in range(wo):
+                        base = f["src"] + r * f["ws_in"] + c * s + off
+                        hs[q, c] = lds[base:base + taps].sum()
             out = np.zeros((ho, wo))
             for r in range(ho):
                 out[r] = hs[r * s:r * s + taps].sum(0)
             out = f["weight"] * out + f["bias"]
+            if reduce and stage.pairs <= 2:
+                # a one-pair reduction leaves its two wave partial sums at cgp_net_args.hs
+                flat = src.reshape(-1)
+                lds[stage.hs] = flat[np.arange(flat.size) % 128 < 64].sum() + 1.0
+                lds[stage.hs + 1] = flat[np.arange(flat.size) % 128 >= 64].sum() + 1.0
             if f.get("relu"):
                 vx, vy = var[v]
                 out = _relu(out, vx[i], vy[j])
@@ -123,7 +148,6 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
             if f.get("dst2", -1) >= 0:
                 vx, vy = var[f["var2"]]
                 lds[plane(f["dst2"], ho, wo, f["ws_out"])] = _relu(out, vx[i], vy[j])
-            lds[hs0:hs0 + 2] = 0.0
         elif kind == 1:                                         # RELU
             h, w = f["h"], f["w"]
             vx, vy = var[v]

@@ -8,9 +8,11 @@ O=gpurun_out/r3e
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
+CNNGP_LIB=$PWD/cnn-gp_amd/lib/var/lib_adaptmp.so timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_multi.py tests/test_gpu_fullgeom.py -q -x -k "netfuse or e2e or bench_geometry or world2 or full_scale" --timeout 200 --timeout-method thread > $O/ab_pytest_adaptmp.log 2>&1 || { echo "pytest adaptmp failed"; tail -20 $O/ab_pytest_adaptmp.log; exit 1; }
+echo "adaptmp: $(tail -1 $O/ab_pytest_adaptmp.log)"
 for rep in 1 2; do
   for data in rand mnist; do
-    for v in noadapt adapt3; do
+    for v in noadapt default adaptmp; do
       echo "== $v data=$data rep=$rep"
       CNNGP_LIB=$PWD/cnn-gp_amd/lib/var/lib_$v.so timeout -k 10 200 python tools/netbench.py --data $data --configs mnist_paper_convnet_gp,mnist_paper_residual_cnn_gp,mnist_as_tf,cifar10 2>&1 | grep -v amdgpu.ids || exit 1
     done
