@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 7
+CGP_ABI_VERSION = 8
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -95,7 +95,7 @@ class NetArgs(ctypes.Structure):
         ("nops", _i32), ("channels", _i32), ("h", _i32), ("w", _i32),
         ("same", _i32), ("final_slot", _i32), ("hs", _i32), ("lds_elems", _i32),
         ("flags", _i32), ("pairs", _i32), ("unit_begin", _i64), ("unit_end", _i64),
-        ("final_stage", _i32), ("program", _i32),
+        ("final_stage", _i32), ("program", _i32), ("part", _i32),
     ]
 
 

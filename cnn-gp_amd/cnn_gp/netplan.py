@@ -92,7 +92,7 @@ class Stage:
     final: bool
     load_stride: int                   # elements per unit of the incoming state record
     store_stride: int                  # ... of the outgoing one
-    hs: int = 0                        # LDS cell of a one-pair reduction's partial sums
+    part: int = 0                      # LDS cell of a one-pair reduction's partial sums
 
     @property
     def n_ops(self):
@@ -507,7 +507,7 @@ class NetPlan:
                 raise Unsupported(f"LDS footprint {top * itemsize} B")
         return Stage(records=recs, lds_elems=top, final_slot=final_origin, pairs=pairs,
                      final=final, load_stride=load_stride, store_stride=store_stride,
-                     hs=hs_part)
+                     part=hs_part)
 
     def _hs_cells(self, f):
         """(zero cells, data cells) a separable conv's row pass leaves in the row-sum
@@ -525,7 +525,7 @@ class NetPlan:
         return zero, set(range(q0 * wo, q1 * wo))
 
     def _reduce_cells(self, recs):
-        """Where a one-pair full-map reduction puts its two wave partial sums (cgp_net_args.hs):
+        """Where a one-pair full-map reduction puts its two wave partial sums (cgp_net_args.part):
         inside the data rows of every separable conv's row-sum scratch, which each row pass
         rewrites anyway — so the partials never land on a zero row; 0 without separable
         convs."""
@@ -672,7 +672,8 @@ class NetPlan:
             a.ops = ops_dev.data_ptr()
             a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
             a.nops, a.channels, a.h, a.w = st.n_ops, x.shape[1], x.shape[2], x.shape[3]
-            a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, st.hs, st.lds_elems
+            a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, 0, st.lds_elems
+            a.part = st.part
             a.flags = flags | (N.CGP_FLAG_NET_DUAL if st.dual else 0)
             a.pairs = st.pairs
             a.final_stage = int(st.final)

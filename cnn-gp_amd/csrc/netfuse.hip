@@ -273,7 +273,7 @@ struct NetP {
     unsigned long long* work;   // per-XCD unit counters (CGP_NET_DYN), zeroed per launch
     long long ldo, units, ubeg, uend;
     unsigned n1, n2, nbi, nbj;
-    int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact, final_stage;
+    int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact, final_stage, part;
 };
 
 // The pairs an op works on.  NP == 1: (i, j), uniform.  NP > 1: pair q of the group is
@@ -480,7 +480,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             }
         }
         acc = wave_sum(acc);
-        T* part = lds + p.hs;
+        T* part = lds + p.part;   // off the scratch's zero rows (cgp_net_args.part)
         if ((tid & 63) == 0) part[tid >> 6] = acc;
         lds_barrier();
         if (tid == 0) {
@@ -1466,7 +1466,7 @@ int net_impl(const cgp_net_args* a, void* stream) {
     if (a->lds_elems <= 0 || lds_bytes > 160 * 1024)
         return fail(CGP_EINVAL, "net: LDS footprint %lld bytes out of range", lds_bytes);
     if (a->final_slot < 0 || a->final_slot >= a->lds_elems || a->hs < 0 ||
-        a->hs >= a->lds_elems)
+        a->hs >= a->lds_elems || a->part < 0 || a->part + 2 > a->lds_elems)
         return fail(CGP_EINVAL, "net: slot offsets out of range");
     NetP<T> p;
     p.x = static_cast<const T*>(a->x);
@@ -1489,6 +1489,7 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.same = a->same;
     p.final_slot = a->final_slot;
     p.hs = a->hs;
+    p.part = a->part;
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
     const int np = a->pairs <= 0 ? 1 : a->pairs;

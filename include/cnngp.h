@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 7
+#define CGP_ABI_VERSION 8
 
 /* error codes */
 #define CGP_OK 0
@@ -307,6 +307,9 @@ typedef struct cgp_net_args {
     int32_t final_stage;   /* 1: write K (the last stage); 0: the ops end in CGP_NET_STORE */
     int32_t program;       /* 0: interpret the op records; k > 0: run compiled program k,
                               the value cgp_net_program() returned for these records */
+    int32_t part;          /* LDS offset of the two wave partial sums of a one-pair
+                              full-map reduction (ABI 8): cells the host keeps off the
+                              scratch's zero rows (CGP_NET_CODE_HS_CLEAN) */
 } cgp_net_args;
 
 /*

@@ -135,10 +135,10 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
                 out[r] = hs[r * s:r * s + taps].sum(0)
             out = f["weight"] * out + f["bias"]
             if reduce and stage.pairs <= 2:
-                # a one-pair reduction leaves its two wave partial sums at cgp_net_args.hs
+                # a one-pair reduction leaves its two wave partial sums at cgp_net_args.part
                 flat = src.reshape(-1)
-                lds[stage.hs] = flat[np.arange(flat.size) % 128 < 64].sum() + 1.0
-                lds[stage.hs + 1] = flat[np.arange(flat.size) % 128 >= 64].sum() + 1.0
+                lds[stage.part] = flat[np.arange(flat.size) % 128 < 64].sum() + 1.0
+                lds[stage.part + 1] = flat[np.arange(flat.size) % 128 >= 64].sum() + 1.0
             if f.get("relu"):
                 vx, vy = var[v]
                 out = _relu(out, vx[i], vy[j])
