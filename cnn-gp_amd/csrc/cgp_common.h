@@ -418,18 +418,88 @@ __device__ __forceinline__ cgp_f2 relu_fast2(cgp_f2 c, cgp_f2 v1, cgp_f2 v2) {
     const cgp_f2 hpos = (c + ac) * cgp_f2(0.25f);              // max(c, 0) / 2
     return __builtin_elementwise_fma((st * x) * sx, p, hpos);
 }
-template <int R>
+// relu_fast's steps before / after the polynomial, packed (two pixels) and scalar: x, the
+// factor m = (sqrt(t)·x)·sqrt(x) and max(c, 0)/2, then out = m·P(x) + max(c, 0)/2 — the
+// same IEEE operations in the same order as relu_fast2 / relu_fast
+__device__ __forceinline__ void relu_prep2(cgp_f2 c, cgp_f2 v1, cgp_f2 v2, cgp_f2& x, cgp_f2& m,
+                                           cgp_f2& hpos) {
+    const cgp_f2 t = __builtin_elementwise_fma(v1, v2, cgp_f2(K<float>::tiny));
+    const cgp_f2 y = {__builtin_amdgcn_rsqf(t.x), __builtin_amdgcn_rsqf(t.y)};
+    const cgp_f2 st = t * y;
+    const cgp_f2 cy = c * y;
+    const cgp_f2 a = {__builtin_fminf(__builtin_fabsf(cy.x), 1.0f),
+                      __builtin_fminf(__builtin_fabsf(cy.y), 1.0f)};
+    x = __builtin_elementwise_fma(cgp_f2(-0.5f), a, cgp_f2(0.5f));
+    const cgp_f2 xm = {__builtin_fmaxf(x.x, K<float>::xfloor), __builtin_fmaxf(x.y, K<float>::xfloor)};
+    const cgp_f2 h = {__builtin_amdgcn_rsqf(xm.x), __builtin_amdgcn_rsqf(xm.y)};
+    m = (st * x) * (xm * h);
+    const cgp_f2 ac = {__builtin_fabsf(c.x), __builtin_fabsf(c.y)};
+    hpos = (c + ac) * cgp_f2(0.25f);
+}
+__device__ __forceinline__ void relu_prep1(float c, float v1, float v2, float& x, float& m,
+                                           float& hpos) {
+    const float t = __builtin_fmaf(v1, v2, K<float>::tiny);
+    const float y = __builtin_amdgcn_rsqf(t);
+    const float st = t * y;
+    const float a = __builtin_fminf(__builtin_fabsf(c * y), 1.0f);
+    x = __builtin_fmaf(-0.5f, a, 0.5f);
+    const float xm = __builtin_fmaxf(x, K<float>::xfloor);
+    m = (st * x) * (xm * __builtin_amdgcn_rsqf(xm));
+    hpos = (c + __builtin_fabsf(c)) * 0.25f;
+}
+// R pixels (packed pairs + an odd scalar one) through the degree-D Horner of P
+template <int R, int D>
+__device__ __forceinline__ void relu_poly_f(const float (&P)[D + 1], float (&c)[R],
+                                            const cgp_f2 (&x2)[R / 2 + 1],
+                                            const cgp_f2 (&m2)[R / 2 + 1],
+                                            const cgp_f2 (&h2)[R / 2 + 1], float xs, float ms,
+                                            float hs) {
+#pragma unroll
+    for (int q = 0; q < R / 2; ++q) {
+        cgp_f2 p = cgp_f2(P[D]);
+#pragma unroll
+        for (int k = D - 1; k >= 0; --k) p = __builtin_elementwise_fma(p, x2[q], cgp_f2(P[k]));
+        const cgp_f2 o = __builtin_elementwise_fma(m2[q], p, h2[q]);
+        c[2 * q] = o.x;
+        c[2 * q + 1] = o.y;
+    }
+    if constexpr (R % 2) {
+        float p = P[D];
+#pragma unroll
+        for (int k = D - 1; k >= 0; --k) p = __builtin_fmaf(p, xs, P[k]);
+        c[R - 1] = __builtin_fmaf(ms, p, hs);
+    }
+}
+// AD (one-pair code, CGP_RELU_ADAPT): the shortest float polynomial whose interval holds
+// every active lane's pixels of the wave (kReluAdaptF*: degrees 3 / 5 on x <= 1/8 / 3/8
+// at the degree-6 fit's bound)
+template <int R, bool AD = false>
 __device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],
                                             const float (&v2)[R], const PolyTab& tab) {
 #if CGP_F32_PACKED
+    cgp_f2 x2[R / 2 + 1], m2[R / 2 + 1], h2[R / 2 + 1];
+    float xs = 0.0f, ms = 0.0f, hs = 0.0f;
 #pragma unroll
-    for (int r = 0; r + 1 < R; r += 2) {
-        const cgp_f2 o = relu_fast2(cgp_f2{c[r], c[r + 1]}, cgp_f2{v1[r], v1[r + 1]},
-                                    cgp_f2{v2[r], v2[r + 1]});
-        c[r] = o.x;
-        c[r + 1] = o.y;
+    for (int q = 0; q < R / 2; ++q)
+        relu_prep2(cgp_f2{c[2 * q], c[2 * q + 1]}, cgp_f2{v1[2 * q], v1[2 * q + 1]},
+                   cgp_f2{v2[2 * q], v2[2 * q + 1]}, x2[q], m2[q], h2[q]);
+    if constexpr (R % 2) relu_prep1(c[R - 1], v1[R - 1], v2[R - 1], xs, ms, hs);
+#if CGP_RELU_ADAPT
+    if constexpr (AD) {
+        float xmax = (R % 2) ? xs : 0.0f;
+#pragma unroll
+        for (int q = 0; q < R / 2; ++q) xmax = __builtin_fmaxf(xmax, __builtin_fmaxf(x2[q].x, x2[q].y));
+        if (__all(xmax <= kReluAdaptFX0)) {
+            relu_poly_f<R, kReluAdaptFDeg0>(kReluAdaptFP0, c, x2, m2, h2, xs, ms, hs);
+        } else if (__all(xmax <= kReluAdaptFX1)) {
+            relu_poly_f<R, kReluAdaptFDeg1>(kReluAdaptFP1, c, x2, m2, h2, xs, ms, hs);
+        } else {
+            relu_poly_f<R, kReluPolyDegF>(kReluPolyF, c, x2, m2, h2, xs, ms, hs);
+        }
+        return;
     }
-    if constexpr (R % 2) c[R - 1] = relu_fast(c[R - 1], v1[R - 1], v2[R - 1], tab);
+#endif
+    relu_poly_f<R, kReluPolyDegF>(kReluPolyF, c, x2, m2, h2, xs, ms, hs);
 #else
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = relu_fast(c[r], v1[r], v2[r], tab);

@@ -321,7 +321,7 @@ __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2
     } else if constexpr (sizeof(T) == 8) {
         relu_q_n<R, QIN, AD>(v, u1, u2, tab, seg);
     } else {
-        relu_fast_n<R>(v, u1, u2, tab);
+        relu_fast_n<R, AD == 1>(v, u1, u2, tab);
     }
 }
 

@@ -118,6 +118,8 @@ def check(monox, dt, npts=20001, xmax=0.5):
 # range-adaptive ReLU (CGP_RELU_ADAPT): lower degrees on sub-intervals [0, xmax] with the
 # same 1.6e-14 bound, taken by a wave whose every pixel has x <= xmax (relu_q_n)
 ADAPT = ((0.125, 7), (0.25, 9), (0.375, 11))
+# ... and for the float polynomial (its bound: the degree-6 fit's 7.9e-8)
+ADAPT_F = ((0.125, 3), (0.375, 5))
 
 
 def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
@@ -131,6 +133,8 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
         dbl[d] = check(to_x(fit(d)), np.float64, npts=4001)
     sub = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
            for xm, d in ADAPT]
+    sub_f = [(xm, d, check(to_x(fit(d, xm), xm), np.float32, npts=4001, xmax=xm))
+             for xm, d in ADAPT_F]
     lines = [
         "// relu_poly.h - generated by tools/fit_relu_poly.py --write (do not edit by hand).",
         "// P(x), x = (1 - |rho|)/2 in [0, 1/2], monomials in x; the fast ReLU covariance map is",
@@ -156,6 +160,13 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
                   f"constexpr int kReluAdaptDeg{k} = {d};",
                   f"constexpr double kReluAdaptP{k}[{d + 1}] = {{"]
         lines += [f"    {float(c)!r}," for c in cfs]
+        lines += ["};"]
+    for k, (xm, d, (err, cfs)) in enumerate(sub_f):
+        lines += [f"// float, x in [0, {xm}]: degree {d}, max rel err {err:.2e}",
+                  f"constexpr float kReluAdaptFX{k} = {xm!r}f;",
+                  f"constexpr int kReluAdaptFDeg{k} = {d};",
+                  f"constexpr float kReluAdaptFP{k}[{d + 1}] = {{"]
+        lines += [f"    {float(c)!r}f," for c in cfs]
         lines += ["};"]
     lines += [f"constexpr int kReluPolyDegF = {deg_f};",
               f"constexpr float kReluPolyF[{deg_f + 1}] = {{"]
