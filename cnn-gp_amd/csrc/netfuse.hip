@@ -310,6 +310,11 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
 template <typename T, bool EX>
 constexpr bool kQuarter = !EX && sizeof(T) == 8;
 
+// the fp32 closed form's adaptive polynomial measured neutral (the fp32 kernel is bound by
+// its per-op latency chain, not by issue; profiles/r3/ab_r3f_relu_adapt_f32.log): off
+#ifndef CGP_RELU_ADAPT_F32
+#define CGP_RELU_ADAPT_F32 0
+#endif
 // R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4; AD: the caller's
 // waves hold one pair's pixels, so the fp64 form may take the range-adaptive polynomial)
 template <bool EXACT, bool QIN, typename T, int R, int AD = 0>
@@ -321,7 +326,7 @@ __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2
     } else if constexpr (sizeof(T) == 8) {
         relu_q_n<R, QIN, AD>(v, u1, u2, tab, seg);
     } else {
-        relu_fast_n<R, AD == 1>(v, u1, u2, tab);
+        relu_fast_n<R, AD == 1 && CGP_RELU_ADAPT_F32>(v, u1, u2, tab);
     }
 }
 
