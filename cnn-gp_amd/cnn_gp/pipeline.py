@@ -123,6 +123,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                                   dtype=dtype)
     _sync(dev)
     t_kxx = time.perf_counter() - t0
+    if warming is not None:           # done long before on a full-size build; its 1.2 GB
+        warming.join()                # identity must not count in the next phase's peak
+        warming = None
     if dev.type == "cuda":
         res["peak_bytes_kxx_build"] = int(torch.cuda.max_memory_allocated(dev))
         torch.cuda.reset_peak_memory_stats(dev)      # next: the gather and the solve
@@ -150,8 +153,6 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     alpha = None
     t2 = time.perf_counter()
     if rank == dst:
-        if warming is not None:
-            warming.join()
         t2 = time.perf_counter()
         Kd = K if K.dtype == out_dtype else conv(K)
         del K
