@@ -50,7 +50,7 @@ def _fns():
     return kern, solve, scores
 
 
-def _run(world, rank, port, q, gather):
+def _run(world, rank, port, q, gather, dst=0):
     import sys
     from conftest import PKG, ROOT
     sys.path[:0] = [PKG, ROOT]
@@ -63,8 +63,8 @@ def _run(world, rank, port, q, gather):
         X, Z, Y = _data()
         kern, solve, scores = _fns()
         res = classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B, device="cpu",
-                                   gather_kxz=gather)
-        if rank == 0:
+                                   gather_kxz=gather, dst=dst)
+        if rank == dst:
             # numpy: pickled by value (a torch tensor on an mp queue travels as a shared
             # memory handle, which dies with this process)
             out = {k: (res[k].numpy() if isinstance(res[k], torch.Tensor) else res[k])
@@ -79,13 +79,15 @@ def _run(world, rank, port, q, gather):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,gather", [(2, True), (3, False), (3, True)])
-def test_gloo_pipeline_matches_single_process(world, gather):
+@pytest.mark.parametrize("world,gather,dst", [(2, True, 0), (3, False, 0), (3, True, 0),
+                                              (3, True, 2)])
+def test_gloo_pipeline_matches_single_process(world, gather, dst):
     single = _run(1, 0, None, None, True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(world, r, port, q, gather)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(world, r, port, q, gather, dst))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
