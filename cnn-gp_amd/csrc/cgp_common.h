@@ -309,9 +309,24 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 // sqrt(t) = T·r·(3 − T·r·r), and |cq|·Y = |c|/sqrt(t) = |rho|.  With x4 = 4x = 2 − 2|rho|,
 // 4·sqrt(x) = x4·h·(3 − x4·h·h), h = rsq(x4), the polynomial term is
 // sqrt(t)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/16 at x4/4, and max(c, 0)/2 = cq + |cq|.
+// CGP_HORNER_ASM (A/B option): the whole chain as one inline-asm block (horner_asm.h,
+// tools/gen_horner_asm.py) — one asm per FMA makes the compiler pad every step boundary
+// with an s_nop, since it cannot see inside the blocks
+#ifndef CGP_HORNER_ASM
+#define CGP_HORNER_ASM 0
+#endif
+#if CGP_HORNER_ASM
+#include "horner_asm.h"
+#endif
 // R interleaved Horner chains of degree D with SGPR coefficients t[0..D]
 template <int R, int D>
 __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], ConstD t) {
+#if CGP_HORNER_ASM
+    if constexpr ((R == 7 || R == 4 || R == 3) && (D == 7 || D == 9 || D == 11 || D == 13)) {
+        horner_asm<R, D>(p, u, t);
+        return;
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) p[r] = fma_sc(t[D], u[r], t[D - 1]);
 #pragma unroll
