@@ -151,16 +151,21 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     res["plan_kxz"] = plan_z
     z0, z1 = plan_z[rank]
     alpha = None
-    t2 = time.perf_counter()
+    failure = None
     if rank == dst:
         t2 = time.perf_counter()
         Kd = K if K.dtype == out_dtype else conv(K)
         del K
-        alpha = solve(Kd, Y.to(dev, out_dtype))
+        try:
+            alpha = solve(Kd, Y.to(dev, out_dtype))
+        except Exception as e:      # e.g. LinAlgError (not PD): the other ranks must not
+            failure = e             # wait for an α that never comes (see step 4)
         _sync(dev)
         res["solve_s"] = round(time.perf_counter() - t2, 3)
         say(f"  solve {res['solve_s']:.2f} s")
         res["K"] = Kd
+        if failure is not None and not multi:
+            raise failure
     if dev.type == "cuda":
         res["peak_bytes_gather_solve"] = int(torch.cuda.max_memory_allocated(dev))
         torch.cuda.reset_peak_memory_stats(dev)      # next: the Kxz strips
@@ -177,8 +182,17 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     res["kxz_pairs_rank"] = pz
     done = time.perf_counter() - t0
 
-    # 4. α to every rank, local scores, scores to dst
+    # 4. α to every rank, local scores, scores to dst.  The solve's outcome travels first, so
+    # a failed solve raises on every rank instead of leaving them in the broadcast
     ncls = Y.shape[1] if Y.dim() > 1 else 1
+    if multi:
+        ok = torch.tensor([0 if failure is None else 1], dtype=torch.int64,
+                          device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        dist.broadcast(ok, dst, group=group)
+        if int(ok) != 0 and failure is None:
+            raise RuntimeError(f"classify_distributed: the solve failed on rank {dst}")
+    if failure is not None:
+        raise failure
     if multi:
         if rank != dst:
             alpha = torch.empty((n, ncls), dtype=out_dtype, device=dev)

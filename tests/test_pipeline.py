@@ -171,3 +171,46 @@ def test_strip_plan_weights_zero_share_for_the_solving_rank():
     plan = strip_plan(10000, 60000, 3, weights=[0.5, 1, 1])
     rows = [b - a for a, b in plan]
     assert abs(rows[0] - 2000) <= 8 and abs(rows[1] - 4000) <= 8
+
+
+def _run_not_pd(world, rank, port, q):
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [PKG, ROOT]
+    from cnn_gp.pipeline import classify_distributed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X, Z, Y = _data()
+        kern, _, scores = _fns()
+
+        def solve(K, Y):                     # an indefinite system, as scipy reports it
+            raise np.linalg.LinAlgError("not positive definite")
+
+        try:
+            classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B, device="cpu")
+            q.put((rank, "no error"))
+        except np.linalg.LinAlgError:
+            q.put((rank, "LinAlgError"))
+        except RuntimeError as e:
+            q.put((rank, "RuntimeError" if "solve failed" in str(e) else repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_pipeline_failed_solve_raises_on_every_rank():
+    """a solve that fails on rank 0 (Kxx not positive definite) must not leave the other
+    ranks waiting for α: rank 0 re-raises, the others raise RuntimeError"""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_not_pd, args=(world, r, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == {0: "LinAlgError", 1: "RuntimeError", 2: "RuntimeError"}
