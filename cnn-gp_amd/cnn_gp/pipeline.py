@@ -31,7 +31,43 @@ import torch.distributed as dist
 
 from .gram import gather_strips, gram_strip, strip_cost, strip_plan
 
-__all__ = ("classify_distributed", "kxz_weights")
+__all__ = ("classify_distributed", "kxz_weights", "widening_matrix", "widen_in_place")
+
+
+def widening_matrix(n: int, n2: int, dtype=torch.float32, out_dtype=torch.float64,
+                    device=None):
+    """An [n, n2] ``dtype`` matrix stored in the back half of an [n, n2] ``out_dtype``
+    buffer (out_dtype twice as wide), so widen_in_place can turn it into the wide matrix
+    without a second copy: classify_gp.py:45-48 widens the float32 K to float64 for the
+    solve, and rank 0 then holds 1.0× the float64 matrix instead of 1.5×.
+    Returns (buf, narrow view)."""
+    a, b = torch.empty((), dtype=dtype).element_size(), \
+        torch.empty((), dtype=out_dtype).element_size()
+    if b != 2 * a:
+        raise ValueError(f"{out_dtype} is not twice as wide as {dtype}")
+    buf = torch.empty((n, n2), dtype=out_dtype, device=device)
+    return buf, buf.view(-1).view(dtype)[n * n2:].view(n, n2)
+
+
+def widen_in_place(buf: torch.Tensor, narrow: torch.Tensor,
+                   cast: Optional[Callable] = None, tail_rows: int = 64) -> torch.Tensor:
+    """Convert widening_matrix's narrow rows into buf, front to back.  Row block [i0, i1)
+    is cast in one call when its wide destination ends before its narrow source starts
+    (2·i1 ≤ n + i0; rows ≥ i1 are never touched) — half the rows, then a quarter, … — and
+    the last ``tail_rows`` rows go through a small temporary.  ``cast(src, dst)`` converts
+    one non-overlapping block (default dst.copy_(src); the device path passes
+    solve.cast_into, the HIP cgp_cast_f32_f64).  Returns buf."""
+    cast = cast or (lambda s, d: d.copy_(s))
+    n = buf.shape[0]
+    i0 = 0
+    while i0 < n:
+        i1 = (n + i0) // 2
+        if i1 - i0 < tail_rows:
+            cast(narrow[i0:].clone(), buf[i0:])
+            break
+        cast(narrow[i0:i1], buf[i0:i1])
+        i0 = i1
+    return buf
 
 
 def kxz_weights(world: int, n: int, m: int, kernel_pairs_per_s: float,
@@ -78,7 +114,7 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          device=None, dtype=torch.float64, out_dtype=torch.float64,
                          gather_kxz: bool = False, kxz_share=None, solve_tflops: float = 30.0,
                          widen: Optional[Callable] = None, log: Optional[Callable] = None,
-                         warm: Optional[Callable] = None):
+                         warm: Optional[Callable] = None, cast: Optional[Callable] = None):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
 
@@ -87,7 +123,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     ``dtype``: the kernel's output dtype (K is stored in it; float32 as the reference's
     save_kernel.py stores it); ``out_dtype``: the dtype solve and scores receive (float64:
     classify_gp.py:45-48 widens K) — ``widen(t)`` converts (default ``t.to(out_dtype)``;
-    it may release its input).  ``warm()`` (optional) runs on ``dst`` before the Kxx build
+    it may release its input).  When out_dtype is twice as wide as dtype (float32 → float64),
+    dst's K lives in the back half of the wide matrix and is widened in place
+    (widen_in_place with ``cast(src, dst)``, default a torch copy).  ``warm()`` (optional) runs on ``dst`` before the Kxx build
     and may return a thread to join before the solve (solve.warm_up_solver: the solver
     libraries load while the kernels run).  Returns on ``dst`` a dict with alpha, scores, pred, K (the
     matrix solve saw), Kxz (when gather_kxz), dst's own Kxz rows (``kxz_rows``,
@@ -114,9 +152,16 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     t0 = time.perf_counter()
     warming = warm() if (warm is not None and rank == dst) else None
     r0, r1 = plan_x[rank]
-    K = None
+    K = Kwide = None
+    in_place = dtype != out_dtype and \
+        2 * torch.empty((), dtype=dtype).element_size() == \
+        torch.empty((), dtype=out_dtype).element_size()
     if rank == dst:
-        K = torch.full((n, n), float("nan"), dtype=dtype, device=dev)
+        if in_place:
+            Kwide, K = widening_matrix(n, n, dtype, out_dtype, dev)
+            K.fill_(float("nan"))
+        else:
+            K = torch.full((n, n), float("nan"), dtype=dtype, device=dev)
         _, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), out=K[r0:r1], dtype=dtype)
     else:
         strip, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), device=dev,
@@ -154,8 +199,13 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     failure = None
     if rank == dst:
         t2 = time.perf_counter()
-        Kd = K if K.dtype == out_dtype else conv(K)
-        del K
+        if K.dtype == out_dtype:
+            Kd = K
+        elif Kwide is not None:
+            Kd = widen_in_place(Kwide, K, cast)
+        else:
+            Kd = conv(K)
+        del K, Kwide
         try:
             alpha = solve(Kd, Y.to(dev, out_dtype))
         except Exception as e:      # e.g. LinAlgError (not PD): the other ranks must not

@@ -15,7 +15,8 @@ import torch
 from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
-           "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores")
+           "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores",
+           "cast_into")
 
 
 def _device():
@@ -159,6 +160,20 @@ def load_kern(dset, i, device=None):
         out = torch.empty(src.shape, dtype=torch.float64, device=dev)
         N.call("cgp_cast_f32_f64", N.ptr(src), N.ptr(out), src.numel(), _stream(dev))
     return out
+
+
+def cast_into(src, dst):
+    """dst (float64) ← src (float32), same shape, both contiguous on one device, through
+    cgp_cast_f32_f64 (classify_gp.py:45-48's widening of the stored float32 K); the two
+    ranges must not overlap (pipeline.widen_in_place guarantees it)."""
+    if src.dtype != torch.float32 or dst.dtype != torch.float64 or \
+            src.shape != dst.shape or src.device != dst.device or \
+            not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("cast_into: contiguous float32 src and float64 dst of one shape "
+                         "on one device")
+    with torch.cuda.device(dst.device):
+        N.call("cgp_cast_f32_f64", N.ptr(src), N.ptr(dst), src.numel(), _stream(dst.device))
+    return dst
 
 
 def scores(Kxz, A):

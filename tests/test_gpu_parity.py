@@ -624,6 +624,21 @@ def test_predict_and_cast():
     np.testing.assert_array_equal(out.cpu().numpy(), f32[1].astype(np.float64))
 
 
+@pytest.mark.parametrize("n,n2", [(1, 1), (65, 65), (700, 130), (3001, 3001)])
+def test_widen_in_place_on_device(n, n2):
+    """pipeline.widen_in_place through the HIP cast (cnn_gp.cast_into): the float32 matrix
+    in the back half of the float64 buffer comes out widened exactly"""
+    from cnn_gp.pipeline import widen_in_place, widening_matrix
+    buf, k32 = widening_matrix(n, n2, device=DEV)
+    src = torch.randn(n, n2, dtype=torch.float32, device=DEV)
+    k32.copy_(src)
+    widen_in_place(buf, k32, cnn_gp.cast_into)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, src.double())
+    with pytest.raises(ValueError):
+        cnn_gp.cast_into(src, torch.empty((n, n2), dtype=torch.float32, device=DEV))
+
+
 def test_concurrent_streams_match():
     """tiles of one Kxx evaluated on two streams at once (about 100 staged launches in
     flight, each with its own per-XCD work counters) equal the one-launch result"""

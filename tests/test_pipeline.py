@@ -50,7 +50,7 @@ def _fns():
     return kern, solve, scores
 
 
-def _run(world, rank, port, q, gather, dst=0):
+def _run(world, rank, port, q, gather, dst=0, dtype=torch.float64):
     import sys
     from conftest import PKG, ROOT
     sys.path[:0] = [PKG, ROOT]
@@ -63,7 +63,7 @@ def _run(world, rank, port, q, gather, dst=0):
         X, Z, Y = _data()
         kern, solve, scores = _fns()
         res = classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B, device="cpu",
-                                   gather_kxz=gather, dst=dst)
+                                   gather_kxz=gather, dst=dst, dtype=dtype)
         if rank == dst:
             # numpy: pickled by value (a torch tensor on an mp queue travels as a shared
             # memory handle, which dies with this process)
@@ -115,6 +115,57 @@ def test_gloo_pipeline_matches_single_process(world, gather, dst):
     A = O.solve_upper(Kref, Y.numpy(), 1e-6)
     Sref = O.kernel(spec, Z.numpy(), X.numpy(), False, False) @ A
     np.testing.assert_allclose(res["scores"], Sref, rtol=1e-6, atol=1e-9)
+
+
+def test_gloo_pipeline_float32_kernels_widened_in_place():
+    """float32 kernels (save_kernel.py's precision) widened to float64 in place on rank 0
+    (pipeline.widen_in_place): K and α bit-equal to the one-process run, and K equal to the
+    float64 kernel rounded to float32"""
+    single = _run(1, 0, None, None, False, 0, torch.float32)
+    assert single["K"].dtype == np.float64
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(world, r, port, q, True, 1, torch.float32))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    iu = np.triu_indices(N)
+    assert np.array_equal(res["K"][iu], single["K"][iu])
+    assert np.array_equal(res["alpha"], single["alpha"])
+    Kref = O.kernel(specs.mnist_paper_convnet_gp(), _data()[0].numpy())
+    assert np.array_equal(res["K"][iu], Kref.astype(np.float32).astype(np.float64)[iu])
+    assert res["Kxz"].dtype == np.float32
+
+
+@pytest.mark.parametrize("n,n2,tail", [(1, 1, 64), (2, 3, 1), (3, 3, 1), (63, 5, 64),
+                                       (64, 64, 1), (65, 7, 64), (1000, 33, 64),
+                                       (1000, 1000, 8), (129, 1, 2)])
+def test_widen_in_place_equals_a_copy(n, n2, tail):
+    """the float32 matrix in the back half of the float64 buffer comes out widened exactly,
+    whatever the block sizes, down to one-row blocks"""
+    from cnn_gp.pipeline import widen_in_place, widening_matrix
+    buf, k32 = widening_matrix(n, n2)
+    assert k32.data_ptr() == buf.data_ptr() + 4 * n * n2 and k32.is_contiguous()
+    src = torch.randn(n, n2, dtype=torch.float32)
+    k32.copy_(src)
+    calls = []
+
+    def cast(s, d):
+        # every block's source and destination are disjoint byte ranges
+        sa, da = s.data_ptr(), d.data_ptr()
+        assert sa >= da + 8 * d.numel() or da >= sa + 4 * s.numel()
+        calls.append(len(s))
+        d.copy_(s)
+
+    out = widen_in_place(buf, k32, cast, tail_rows=tail)
+    assert out is buf and torch.equal(buf, src.double())
+    assert sum(calls) == n
 
 
 @pytest.mark.parametrize("n,n2,world", [(60000, None, 8), (10000, 60000, 8), (50000, None, 8),

@@ -55,12 +55,9 @@ def log(rank, msg):
 
 def widen(t):
     """float32 device matrix -> float64 (classify_gp.py:45-48's load_kern widening, on the
-    device through cgp_cast_f32_f64)."""
-    out = torch.empty(t.shape, dtype=torch.float64, device=t.device)
-    from cnn_gp import _native as N
-    N.call("cgp_cast_f32_f64", N.ptr(t), N.ptr(out), t.numel(),
-           torch.cuda.current_stream(t.device).cuda_stream)
-    return out
+    device through cgp_cast_f32_f64); Kxx itself is widened in place by the pipeline."""
+    return cnn_gp.cast_into(t.contiguous(), torch.empty(t.shape, dtype=torch.float64,
+                                                         device=t.device))
 
 
 def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spot=16,
@@ -112,7 +109,8 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                    gather_kxz=pred_var,
                                    widen=widen if kd != torch.float64 else None,
                                    log=lambda msg: log(rank, msg),
-                                   warm=lambda: cnn_gp.warm_up_solver(dev))
+                                   warm=lambda: cnn_gp.warm_up_solver(dev),
+                                   cast=cnn_gp.cast_into)
     wall = time.perf_counter() - t0
     if rank != 0:
         return None
