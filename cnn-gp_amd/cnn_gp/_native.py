@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 9
+CGP_ABI_VERSION = 8
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -129,7 +129,6 @@ SIGNATURES = {
     "cgp_axpby_f64": (_i32, [_f64, _vp, _f64, _vp, _vp, _i64, _vp]),
     "cgp_axpby_f32": (_i32, [_f64, _vp, _f64, _vp, _vp, _i64, _vp]),
     "cgp_scale_batch_f64": (_i32, [_i32, _vp, _vp, _vp, _f64, _vp]),
-    "cgp_fact_batch_f64": (_i32, [_i32, _vp, _vp, _vp, _vp]),
     "cgp_cast_f32_f64": (_i32, [_vp, _vp, _i64, _vp]),
     "cgp_transpose_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_chol_solve_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,
@@ -141,7 +140,6 @@ SIGNATURES = {
     "cgp_net_hs_elems": (_i32, [_i32]),
     "cgp_net_supertile": (_i32, []),
     "cgp_net_units": (_i32, [_i32]),
-    "cgp_net_fact": (_i32, []),
     "cgp_net_resolution": (_i32, [_i32, _i32]),
     "cgp_net_op_size": (ctypes.c_size_t, []),
     "cgp_net_args_size": (ctypes.c_size_t, []),

@@ -656,24 +656,6 @@ class NetPlan:
                 quarters.append((vx, q))
                 keep.append(q)
                 var[v] = (q, vy)
-        # or, with a library built to read them (cgp_net_fact), factored maps on both sides:
-        # (2/sqrt(v), sqrt(v)) per pixel (relu_qf_n), filled on the launch stream
-        facts = []
-        fused = self.fact_vars(x.dtype, flags)
-        if fused:
-            var = dict(var)
-            for v in sorted(fused):
-                vx, vy = var[v]
-                if not (vx.is_contiguous() and vy.is_contiguous()):
-                    raise ValueError("variance maps must be contiguous")
-                fx = torch.empty(vx.shape + (2,), dtype=vx.dtype, device=vx.device)
-                facts.append((vx, fx))
-                fy = fx
-                if vy.data_ptr() != vx.data_ptr() or vy.shape != vx.shape:
-                    fy = torch.empty(vy.shape + (2,), dtype=vy.dtype, device=vy.device)
-                    facts.append((vy, fy))
-                keep += [vx, vy, fx, fy]
-                var[v] = (fx, fy)
         for sidx, st in enumerate(self.stages):
             arr = self._ops_array(st, var, states[sidx], states[sidx + 1])
             # pinned + non_blocking: a pageable H2D copy would block the host until the
@@ -708,17 +690,9 @@ class NetPlan:
             q_dst = (ctypes.c_void_p * nq)(*[N.ptr(q_) for _, q_ in quarters])
             q_n = (ctypes.c_int64 * nq)(*[s_.numel() for s_, _ in quarters])
 
-        if facts:      # one launch fills every factored map
-            nf = len(facts)
-            f_src = (ctypes.c_void_p * nf)(*[N.ptr(s_) for s_, _ in facts])
-            f_dst = (ctypes.c_void_p * nf)(*[N.ptr(f_) for _, f_ in facts])
-            f_n = (ctypes.c_int64 * nf)(*[s_.numel() for s_, _ in facts])
-
         def run_all(stream):
             if quarters:
                 N.call("cgp_scale_batch_f64", nq, q_src, q_dst, q_n, 0.25, stream)
-            if facts:
-                N.call("cgp_fact_batch_f64", nf, f_src, f_dst, f_n, stream)
             for u0 in range(0, units, chunk):
                 u1 = min(units, u0 + chunk)
                 for a in launches:
@@ -750,25 +724,10 @@ class NetPlan:
 
         return launch, out
 
-    def _closed_form_f64(self, dtype, flags: int) -> bool:
-        return dtype == torch.float64 and not flags & N.CGP_FLAG_EXACT_RELU
-
-    def fact_vars(self, dtype, flags: int = 0) -> set:
-        """Values whose variance maps the fp64 closed-form ReLU reads factored, on both
-        sides (a library built with CGP_RELU_FACT: cgp_net_fact() == 1)."""
-        if not self._closed_form_f64(dtype, flags) or not self._lib.cgp_net_fact():
-            return set()
-        return self._relu_vars()
-
     def quarter_vars(self, dtype, flags: int = 0) -> set:
-        """Values whose x-side variance maps the fp64 closed-form ReLU reads quartered
-        (a library that does not read factored maps)."""
-        if not self._closed_form_f64(dtype, flags) or not QUARTER_MAPS or \
-                self._lib.cgp_net_fact():
+        """Values whose x-side variance maps the fp64 closed-form ReLU reads quartered."""
+        if dtype != torch.float64 or flags & N.CGP_FLAG_EXACT_RELU or not QUARTER_MAPS:
             return set()
-        return self._relu_vars()
-
-    def _relu_vars(self) -> set:
         used = set()
         for st in self.stages:
             used |= {v for _, v in st.records if v is not None}

@@ -341,84 +341,21 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
 // hold the same pair as this lane (multi-pair stages, CGP_RELU_ADAPT_MP), so a pair's
 // polynomial depends on its own pixels only and a wave whose pairs disagree runs each
 // chosen polynomial under its lanes' exec mask
-// Y = 4/sqrt(t) and sqrt(t) of T = t/4 (one Newton step on v_rsq_f64, as above)
-__device__ __forceinline__ void relu_q_scale(double T, double& y, double& st) {
-    const double r0 = __builtin_amdgcn_rsq(T);
-    const double m = T * r0;
-    const double k = __builtin_fma(-m, r0, 3.0);
-    y = r0 * k;
-    st = m * k;
-}
-template <int R, int AD>
-__device__ __forceinline__ void relu_q_tail(double (&c)[R], const double (&y)[R],
-                                            const double (&st)[R], const PolyTab& tab,
-                                            unsigned long long seg);
 template <int R, bool QIN, int AD = 0>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
                                          const double (&v2)[R], const PolyTab& tab,
                                          unsigned long long seg = ~0ull) {
-    double y[R], st[R];
+    double y[R], st[R], sx[R], u[R], p[R];   // u: x4
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if constexpr (!QIN) c[r] *= 0.25;
-        relu_q_scale(__builtin_fma(v1q[r], v2[r], 0.25 * K<double>::tiny), y[r], st[r]);
+        const double T = __builtin_fma(v1q[r], v2[r], 0.25 * K<double>::tiny);
+        const double r0 = __builtin_amdgcn_rsq(T);
+        const double m = T * r0;
+        const double k = __builtin_fma(-m, r0, 3.0);
+        y[r] = r0 * k;
+        st[r] = m * k;
     }
-    relu_q_tail<R, AD>(c, y, st, tab, seg);
-}
-// Factored variances (CGP_RELU_FACT): each side's map holds g = (2/sqrt(v), sqrt(v)) per
-// pixel (cgp_fact_batch_f64, once per image), so Y = 4/sqrt(v1·v2) = g1.x·g2.x and
-// sqrt(t) = g1.y·g2.y cost two multiplies instead of an fma, a v_rsq_f64 and a Newton
-// step.  Exact to rounding wherever the reference's + tiny (f32 tiny, kernels.py ReLU)
-// sits below half an ulp of v1·v2, i.e. sqrt(v1·v2) >= 2^-36; a pixel below that (the
-// zero-variance border of the first layers) takes the unfactored path on T = st²/4 +
-// tiny/4 under its own lane's exec mask, so every pixel's result is its own (independent
-// of the other pixels of its wave)
-constexpr double kFactMin = 0x1p-36;
-typedef double cgp_d2 __attribute__((ext_vector_type(2)));
-// the two factors of a pixel: Y = g1.x·g2.x, sqrt(t) = g1.y·g2.y (the caller multiplies
-// them as soon as both sides' loads are in, so only two values per pixel stay live)
-__device__ __forceinline__ void fact_combine(cgp_d2 g1, cgp_d2 g2, double& y, double& st) {
-    y = g1.x * g2.x;
-    st = g1.y * g2.y;
-}
-template <int R, bool QIN, int AD = 0>
-__device__ __forceinline__ void relu_qf_n(double (&c)[R], const double (&y0)[R],
-                                          const double (&st0)[R], const PolyTab& tab,
-                                          unsigned long long seg = ~0ull) {
-    double y[R], st[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if constexpr (!QIN) c[r] *= 0.25;
-        y[r] = y0[r];
-        st[r] = st0[r];
-    }
-    // a wave-uniform skip first: a per-lane branch alone runs its few instructions with an
-    // empty exec mask rather than jump over them
-#ifndef CGP_FACT_NOSLOW
-    // pixels below kFactMin: the unfactored values, selected per lane (straight-line code
-    // under one wave-uniform branch that the common case skips)
-    bool low = false;
-#pragma unroll
-    for (int r = 0; r < R; ++r) low |= !(st[r] >= kFactMin);
-    if (__any(low)) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const double h = 0.5 * st[r];
-            double ys, ss;
-            relu_q_scale(__builtin_fma(h, h, 0.25 * K<double>::tiny), ys, ss);
-            const bool lo = !(st[r] >= kFactMin);
-            y[r] = lo ? ys : y[r];
-            st[r] = lo ? ss : st[r];
-        }
-    }
-#endif
-    relu_q_tail<R, AD>(c, y, st, tab, seg);
-}
-template <int R, int AD>
-__device__ __forceinline__ void relu_q_tail(double (&c)[R], const double (&y)[R],
-                                            const double (&st)[R], const PolyTab& tab,
-                                            unsigned long long seg) {
-    double sx[R], u[R], p[R];   // u: x4
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const double a = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);

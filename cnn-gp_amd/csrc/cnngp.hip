@@ -724,21 +724,6 @@ __global__ __launch_bounds__(kBlock) void scale_batch_kernel(ScaleBatch b, doubl
         dst[e] = alpha * src[e];
 }
 
-// (2/sqrt(v), sqrt(v)) per element: the factored variance maps of the fp64 closed-form
-// ReLU (cgp_common.h relu_qf_n).  IEEE sqrt and division, so each factor is within an ulp;
-// v = 0 gives (inf, 0) and the ReLU takes its unfactored path there
-__global__ __launch_bounds__(kBlock) void fact_batch_kernel(ScaleBatch b) {
-    const int k = blockIdx.y;
-    const double* __restrict__ src = b.src[k];
-    double2* __restrict__ dst = reinterpret_cast<double2*>(b.dst[k]);
-    const long long n = b.n[k];
-    const long long stride = (long long)gridDim.x * kBlock;
-    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride) {
-        const double s = __dsqrt_rn(src[e]);
-        dst[e] = make_double2(__ddiv_rn(2.0, s), s);
-    }
-}
-
 __global__ __launch_bounds__(kBlock) void cast_kernel(const float* __restrict__ in,
                                                       double* __restrict__ out, long long n) {
     const long long stride = (long long)gridDim.x * kBlock;
@@ -1509,31 +1494,6 @@ int cgp_scale_batch_f64(int32_t count, const double* const* src, double* const* 
         hipLaunchKernelGGL(scale_batch_kernel, dim3(grid_for(most), m), dim3(kBlock), 0,
                            as_stream(stream), b, alpha);
         const int rc = check_launch("scale_batch_kernel");
-        if (rc != CGP_OK) return rc;
-    }
-    return CGP_OK;
-}
-int cgp_fact_batch_f64(int32_t count, const double* const* src, double* const* dst,
-                       const int64_t* n, void* stream) {
-    if (count < 0 || (count > 0 && (!src || !dst || !n)))
-        return fail(CGP_EINVAL, "fact_batch: bad arguments");
-    for (int base = 0; base < count; base += kScaleBatch) {
-        ScaleBatch b{};
-        long long most = 0;
-        const int m = count - base < kScaleBatch ? count - base : kScaleBatch;
-        for (int k = 0; k < m; ++k) {
-            b.src[k] = src[base + k];
-            b.dst[k] = dst[base + k];
-            b.n[k] = n[base + k];
-            if (b.n[k] < 0 || (b.n[k] > 0 && (!b.src[k] || !b.dst[k])) ||
-                ((uintptr_t)b.dst[k] & 15))
-                return fail(CGP_EINVAL, "fact_batch: buffer %d", base + k);
-            if (b.n[k] > most) most = b.n[k];
-        }
-        if (most == 0) continue;
-        hipLaunchKernelGGL(fact_batch_kernel, dim3(grid_for(most), m), dim3(kBlock), 0,
-                           as_stream(stream), b);
-        const int rc = check_launch("fact_batch_kernel");
         if (rc != CGP_OK) return rc;
     }
     return CGP_OK;

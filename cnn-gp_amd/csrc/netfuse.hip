@@ -24,7 +24,6 @@
 
 #include <map>
 #include <mutex>
-#include <type_traits>
 #include <utility>
 #include <algorithm>
 #include <climits>
@@ -310,35 +309,6 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
 // scaled its weight and bias by 1/4 (QIN), a quartered input.
 template <typename T, bool EX>
 constexpr bool kQuarter = !EX && sizeof(T) == 8;
-// CGP_RELU_FACT: the fp64 closed form reads factored variance maps, (2/sqrt(v), sqrt(v))
-// per pixel on both sides (relu_qf_n; the host fills them with cgp_fact_batch_f64 and
-// asks cgp_net_fact() whether this library reads them), instead of v/4 and v
-#ifndef CGP_RELU_FACT
-#define CGP_RELU_FACT 1
-#endif
-template <typename T, bool EX>
-constexpr bool kFact = CGP_RELU_FACT && !EX && sizeof(T) == 8;
-#ifndef CGP_FACT_EARLY
-#define CGP_FACT_EARLY 0
-#endif
-// the element type of a variance map as the ReLU reads it
-template <typename T, bool EX>
-using VarT = std::conditional_t<kFact<T, EX>, cgp_d2, T>;
-// loaded map elements -> what the ReLU takes: (v1q, v2) as loaded, or the factored maps'
-// (Y, sqrt(t)) products
-template <typename T, int R, typename V>
-__device__ __forceinline__ void var_combine(const V (&g1)[R], const V (&g2)[R], T (&u1)[R],
-                                            T (&u2)[R]) {
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        if constexpr (std::is_same_v<V, T>) {
-            u1[k] = g1[k];
-            u2[k] = g2[k];
-        } else {
-            fact_combine(g1[k], g2[k], u1[k], u2[k]);
-        }
-    }
-}
 
 // the fp32 closed form's adaptive polynomial measured neutral (the fp32 kernel is bound by
 // its per-op latency chain, not by issue; profiles/r3/ab_r3f_relu_adapt_f32.log): off
@@ -350,9 +320,7 @@ __device__ __forceinline__ void var_combine(const V (&g1)[R], const V (&g2)[R], 
 template <bool EXACT, bool QIN, typename T, int R, int AD = 0>
 __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
                                        const PolyTab& tab, unsigned long long seg = ~0ull) {
-    if constexpr (kFact<T, EXACT>) {
-        relu_qf_n<R, QIN, AD>(v, u1, u2, tab, seg);   // u1, u2: Y and sqrt(t) (var_combine)
-    } else if constexpr (EXACT) {
+    if constexpr (EXACT) {
 #pragma unroll
         for (int k = 0; k < R; ++k) v[k] = relu_exact_inl(v[k], u1[k], u2[k]);
     } else if constexpr (sizeof(T) == 8) {
@@ -423,16 +391,16 @@ __device__ __forceinline__ GP<char> ubase(const void* p) {
 // register shared by both sides when the offsets are folded), k a compile-time step
 // that lands in the instruction's immediate offset.  Per-lane offsets are 32-bit: the
 // multi-pair maps are at most 32x32, and net_impl bounds n1, n2 so they cannot wrap.
-template <typename V>
+template <typename T>
 struct VarSrc {
     GP<char> x, y;
     unsigned xo, yo;
     bool on;
-    __device__ __forceinline__ V ldx(unsigned px, int k = 0) const {
-        return *(GP<V>)(x + (size_t)(xo + px * (unsigned)sizeof(V)) + k * (int)sizeof(V));
+    __device__ __forceinline__ T ldx(unsigned px, int k = 0) const {
+        return *(GP<T>)(x + (size_t)(xo + px * (unsigned)sizeof(T)) + k * (int)sizeof(T));
     }
-    __device__ __forceinline__ V ldy(unsigned px, int k = 0) const {
-        return *(GP<V>)(y + (size_t)(yo + px * (unsigned)sizeof(V)) + k * (int)sizeof(V));
+    __device__ __forceinline__ T ldy(unsigned px, int k = 0) const {
+        return *(GP<T>)(y + (size_t)(yo + px * (unsigned)sizeof(T)) + k * (int)sizeof(T));
     }
 };
 // UNI: i and j are the same in every lane (one pair per workgroup), so their offsets fold
@@ -440,7 +408,7 @@ struct VarSrc {
 template <typename T, bool UNI>
 __device__ __forceinline__ VarSrc<T> var_maps(const void* vx, const void* vy, bool on,
                                               unsigned i, unsigned j, int hw) {
-    VarSrc<T> r;   // T: the map's element type (VarT)
+    VarSrc<T> r;
     r.on = on;
     r.x = ubase(vx);
     r.y = ubase(vy);
@@ -492,15 +460,14 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
-    using V = VarT<T, EX>;
-    const VarSrc<V> vs0 = var_src<V, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
+    const VarSrc<T> vs0 = var_src<T, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
         if constexpr (NP == 1) {
             return vs0;
         } else {
             unsigned iq, jq;
             pair_q<NP>(pr, q, iq, jq);
-            return var_src<V, false>(op, iq, jq, G::HOWO);
+            return var_src<T, false>(op, iq, jq, G::HOWO);
         }
     };
     const T* __restrict__ src = lds + op.src;
@@ -528,13 +495,11 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             T v[1] = {fma_t(w, tot, b)};
             const int at[1] = {0};
             const bool ok[1] = {true};
-            V g1[1] = {V(1)}, g2[1] = {V(1)};
+            T u1[1] = {T(1)}, u2[1] = {T(1)};
             if (vs0.on) {
-                g1[0] = vs0.ldx(0);
-                g2[0] = vs0.ldy(0);
+                u1[0] = vs0.ldx(0);
+                u2[0] = vs0.ldy(0);
             }
-            T u1[1], u2[1];
-            var_combine(g1, g2, u1, u2);
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::REDUCE) {
@@ -556,24 +521,21 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
         for (int m = TPP / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
         if (lane == 0) {
-            const VarSrc<V> vs = vs_of(q);
+            const VarSrc<T> vs = vs_of(q);
             T v[1] = {fma_t(w, acc, b)};
             const int at[1] = {q * arena};
             const bool ok[1] = {true};
-            V g1[1] = {V(1)}, g2[1] = {V(1)};
+            T u1[1] = {T(1)}, u2[1] = {T(1)};
             if (vs.on) {
-                g1[0] = vs.ldx(0);
-                g2[0] = vs.ldy(0);
+                u1[0] = vs.ldx(0);
+                u2[0] = vs.ldy(0);
             }
-            T u1[1], u2[1];
-            var_combine(g1, g2, u1, u2);
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::POINT) {
         constexpr int N = NP * G::HOWO;
         constexpr int KP = (N + G::NT - 1) / G::NT;
-        V g1[KP], g2[KP];
-        T v[KP];
+        T u1[KP], u2[KP], v[KP];
         int at[KP];
         bool ok[KP];
 #pragma unroll
@@ -583,14 +545,12 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             const int ec = ok[k] ? e : 0;
             const int q = NP == 1 ? 0 : udiv(ec, G::HOWO), pc = ec - q * G::HOWO;
             const int r = udiv(pc, G::WO), c = pc - r * G::WO;
-            const VarSrc<V> vs = vs_of(q);
+            const VarSrc<T> vs = vs_of(q);
             at[k] = q * arena + r * wso + c;
-            g1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : V(1);
-            g2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : V(1);
+            u1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : T(1);
+            u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
             v[k] = fma_t(w, src[q * arena + (r * G::S) * wsi + c * G::S], b);
         }
-        T u1[KP], u2[KP];
-        var_combine(g1, g2, u1, u2);
         net_out<T, EX, DU, KP, NP == 1 ? 1 : 0>(lds, op, v, at, ok, u1, u2, tab);
     } else if constexpr (G::DIRECT) {
         // one pass: item (q, g3, c) sums its WIN3 x TAPS input window straight from the
@@ -598,7 +558,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         // same bits); rows outside the map read as zero, columns outside are the slot's
         // zero halo
         constexpr int NVT = NP * G::NV;
-        V g1[G::KV][G::R3], g2[G::KV][G::R3];
         T u1[G::KV][G::R3], u2[G::KV][G::R3];
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
@@ -606,12 +565,12 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             const int itc = (NVT % G::NT == 0 || it < NVT) ? it : 0;
             const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
             const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
-            const VarSrc<V> vs = vs_of(q);
+            const VarSrc<T> vs = vs_of(q);
 #pragma unroll
             for (int k = 0; k < G::R3; ++k) {
                 const unsigned px0 = (unsigned)(g3 * G::R3 * G::WO + c);
-                g1[kv][k] = vs.on ? vs.ldx(px0, k * G::WO) : V(1);
-                g2[kv][k] = vs.on ? vs.ldy(px0, k * G::WO) : V(1);
+                u1[kv][k] = vs.on ? vs.ldx(px0, k * G::WO) : T(1);
+                u2[kv][k] = vs.on ? vs.ldy(px0, k * G::WO) : T(1);
             }
         }
         // outputs that land on the source (in place, or dst2 on the source) are stored
@@ -648,8 +607,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 for (int k = 0; k < G::R3; ++k) res[kv][k] = fma_t(w, o[k], b);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k)
-                    asm volatile("" : "+v"(g1[kv][k]), "+v"(g2[kv][k]));
-                var_combine(g1[kv], g2[kv], u1[kv], u2[kv]);
+                    asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
             }
         }
         if (hazard) lds_barrier();
@@ -675,7 +633,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         T* __restrict__ hs = lds + p.hs;
         constexpr int NHT = NP * G::NH, NVT = NP * G::NV, NZT = NP * G::NZ;
         // variances of this thread's outputs, in flight during the row pass
-        V g1[G::KV][G::R3], g2[G::KV][G::R3];
         T u1[G::KV][G::R3], u2[G::KV][G::R3];
         if (vs0.on) {
 #pragma unroll
@@ -684,22 +641,19 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 const int itc = (NVT % G::NT == 0 || it < NVT) ? it : 0;
                 const int q = NP == 1 ? 0 : udiv(itc, G::NV), l = itc - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
-                const VarSrc<V> vs = vs_of(q);
+                const VarSrc<T> vs = vs_of(q);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) {
                     const unsigned px0 = (unsigned)(g3 * G::R3 * G::WO + c);
-                    g1[kv][k] = vs.ldx(px0, k * G::WO);
-                    g2[kv][k] = vs.ldy(px0, k * G::WO);
+                    u1[kv][k] = vs.ldx(px0, k * G::WO);
+                    u2[kv][k] = vs.ldy(px0, k * G::WO);
                 }
-#if CGP_FACT_EARLY
-                if constexpr (kFact<T, EX>) var_combine(g1[kv], g2[kv], u1[kv], u2[kv]);
-#endif
             }
         } else {
 #pragma unroll
             for (int kv = 0; kv < G::KV; ++kv)
 #pragma unroll
-                for (int k = 0; k < G::R3; ++k) g1[kv][k] = g2[kv][k] = V(1);
+                for (int k = 0; k < G::R3; ++k) u1[kv][k] = u2[kv][k] = T(1);
         }
         // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
 #pragma unroll
@@ -734,16 +688,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 }
             }
         }
-        if constexpr (kFact<T, EX> && !CGP_FACT_EARLY) {
-            // factored maps: the products now (the loads had the row pass), so two values
-            // per pixel instead of four stay live through the column pass
-#pragma unroll
-            for (int kv = 0; kv < G::KV; ++kv) {
-#pragma unroll
-                for (int k = 0; k < G::R3; ++k) asm volatile("" : "+v"(g1[kv][k]), "+v"(g2[kv][k]));
-                var_combine(g1[kv], g2[kv], u1[kv], u2[kv]);
-            }
-        }
         lds_barrier();
         // column pass + output stage (uniform branches outside the per-pixel loops: each
         // stage is one basic block, so the R3 independent ReLUs interleave)
@@ -760,7 +704,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 // the variances are first needed here: without this fence the compiler
                 // folds u1·u2 (the ReLU's t) into the load block at the op start and
                 // waits for the loads there, before the row pass
-                if constexpr (!kFact<T, EX>) var_combine(g1[kv], g2[kv], u1[kv], u2[kv]);
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
                 T o[G::R3], v[G::R3];
@@ -793,13 +736,12 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     const FastDiv fw{op.div_m, op.div_s, (unsigned)op.w};
     // RELU reads (var_x, var_y) = variances of src (an elementwise ReLU has no dst2);
     // LINEAR may carry a dst2 ReLU with (var2_x, var2_y)
-    using V = VarT<T, EX>;
     auto vs_of = [&](unsigned iq, unsigned jq) {
         return KIND == CGP_NET_RELU
-                   ? var_maps<V, NP == 1>(op.var_x, op.var_y, true, iq, jq, hw)
-                   : var_src<V, NP == 1>(op, iq, jq, hw);
+                   ? var_maps<T, NP == 1>(op.var_x, op.var_y, true, iq, jq, hw)
+                   : var_src<T, NP == 1>(op, iq, jq, hw);
     };
-    const VarSrc<V> vs0 = vs_of(pr.i, pr.j);
+    const VarSrc<T> vs0 = vs_of(pr.i, pr.j);
     // the pair's images (MOMENTS, one pair per half: i, j uniform) as scalar byte bases;
     // pixel offsets stay 32-bit unsigned, so every load is SGPR base + VGPR offset with no
     // 64-bit VALU address arithmetic (an image is at most C·hw·8 bytes)
@@ -812,7 +754,6 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     // waves with no pixel in this pass skip the ReLUs (uniform per wave)
     const bool live = base + (tid & ~63) < n;
     T a[KE], u1[KE], u2[KE];
-    V g1[KE], g2[KE];
     int at[KE];
     bool ok[KE];
 #pragma unroll
@@ -823,14 +764,14 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         const int q = NP == 1 ? 0 : ec / hw, pc = ec - q * hw;
         const int r = W_ ? udiv(pc, W_) : (int)fdiv((unsigned)pc, fw);
         at[k] = q * arena + r * ws + (pc - r * wd);
-        VarSrc<V> vs = vs0;
+        VarSrc<T> vs = vs0;
         if constexpr (NP > 1) {
             unsigned iq, jq;
             pair_q<NP>(pr, q, iq, jq);
             vs = vs_of(iq, jq);
         }
-        g1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : V(1);
-        g2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : V(1);
+        u1[k] = (vs.on && ok[k]) ? vs.ldx((unsigned)pc) : T(1);
+        u2[k] = (vs.on && ok[k]) ? vs.ldy((unsigned)pc) : T(1);
         if constexpr (KIND == CGP_NET_RELU) {
             a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
@@ -845,7 +786,6 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
         }
     }
-    var_combine(g1, g2, u1, u2);
     if constexpr (KIND == CGP_NET_MOMENTS) {
         // the channel mean (x / 1 == x: a uniform branch, so one-channel inputs run no
         // division at all)
@@ -1564,10 +1504,8 @@ int net_impl(const cgp_net_args* a, void* stream) {
         return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * net_units(np));
     // multi-pair stages address a pair's variance maps (<= 8 * threads / np pixels) with
     // 32-bit byte offsets (VarSrc)
-    const long long var_elem = (long long)sizeof(T) *
-        (CGP_RELU_FACT && sizeof(T) == 8 && !(a->flags & CGP_FLAG_EXACT_RELU) ? 2 : 1);
     if (np > 1 && (a->n1 > a->n2 ? a->n1 : a->n2) * (8LL * net_threads(np) / np) *
-                          var_elem >= (1LL << 32))
+                          (long long)sizeof(T) >= (1LL << 32))
         return fail(CGP_EINVAL, "net: %lld images too many for %d pairs per workgroup",
                     (long long)(a->n1 > a->n2 ? a->n1 : a->n2), np);
     if (a->unit_begin == 0 && a->unit_end == 0) {
@@ -1617,7 +1555,6 @@ size_t cgp_net_args_size(void) { return sizeof(cgp_net_args); }
 int cgp_net_supertile(void) { return kST; }
 
 int cgp_net_units(int32_t pairs) { return net_units(pairs <= 0 ? 1 : pairs); }
-int cgp_net_fact(void) { return CGP_RELU_FACT; }
 
 int cgp_net_hs_elems(int32_t code) {
     return (code >= 0 && code < kNumGeo) ? kGeoTable[code].hs_elems : -1;

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 9
+#define CGP_ABI_VERSION 8
 
 /* error codes */
 #define CGP_OK 0
@@ -169,15 +169,6 @@ int cgp_axpby_f32(double alpha, const float* a, double beta, const float* b, flo
  */
 int cgp_scale_batch_f64(int32_t count, const double* const* src, double* const* dst,
                         const int64_t* n, double alpha, void* stream);
-
-/*
- * dst[k] = (2/sqrt(v), sqrt(v)) for each v of src[k] (n[k] elements in, 2·n[k] doubles out,
- * dst 16-byte aligned) for count buffers, one launch per 32.  No reference counterpart: the
- * factored variance maps the fp64 closed-form ReLU of cgp_net_f64 reads on both sides when
- * cgp_net_fact() is 1 (instead of the quartered x-side maps above; cnn_gp/netplan.py).
- */
-int cgp_fact_batch_f64(int32_t count, const double* const* src, double* const* dst,
-                       const int64_t* n, void* stream);
 
 /* load_kern's float32 → float64 widening, classify_gp.py:45-48 */
 int cgp_cast_f32_f64(const float* in, double* out, int64_t n, void* stream);
@@ -391,11 +382,6 @@ int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pai
  * the two-pair head stage, whose workgroup holds CGP_NET_SPLIT one-pair slices (2 in the
  * default build).  A stage needs lds_bytes × cgp_net_units(pairs) <= 160 KB. */
 int cgp_net_units(int32_t pairs);
-/* 1 when cgp_net_f64 without CGP_FLAG_EXACT_RELU reads factored variance maps — both
- * sides' var_x / var_y (and var2_*) point at cgp_fact_batch_f64 output, 16 bytes per pixel
- * — instead of the x-side quartered and the y-side plain maps; 0 otherwise (build option
- * CGP_RELU_FACT) */
-int cgp_net_fact(void);
 /* The compiled program (k > 0) whose op list equals ops[0, nops) (HOST memory) in every
  * field but weight, bias and the variance / state pointers, for `pairs` pairs per
  * workgroup, flags (CGP_FLAG_NET_DUAL), the per-pair LDS footprint and the item size
