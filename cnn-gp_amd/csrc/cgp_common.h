@@ -185,9 +185,9 @@ static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 // ADAPT), quartered like kReluPolyTabDq.  relu_q_n takes the shortest one whose interval
 // holds every active lane's pixels of the wave (a wave-uniform branch).  Deep layers have
 // |rho| near 1 (x small): on MNIST-like pairs the ConvNet's ReLUs 2-7 have x <= 0.24 and its
-// last four x <= 0.125.  Only one-pair code uses it (AD in relu_n): there a
-// wave holds one pair's pixels, so a pair's result never depends on the other pairs of
-// its tile; multi-pair stages keep the full polynomial.
+// last four x <= 0.125.  One-pair code votes over the wave (AD 1 in relu_n):
+// there a wave holds one pair's pixels, so a pair's result never depends on the other
+// pairs of its tile; multi-pair stages vote per pair segment (AD 2, CGP_RELU_ADAPT_MP).
 #ifndef CGP_RELU_ADAPT
 #define CGP_RELU_ADAPT 1
 #endif
@@ -209,18 +209,55 @@ static __constant__ AdaptCoef<kReluAdaptDeg0> kReluAdaptTab0 = adapt_coef<kReluA
 static __constant__ AdaptCoef<kReluAdaptDeg1> kReluAdaptTab1 = adapt_coef<kReluAdaptDeg1>(kReluAdaptP1);
 static __constant__ AdaptCoef<kReluAdaptDeg2> kReluAdaptTab2 = adapt_coef<kReluAdaptDeg2>(kReluAdaptP2);
 
+// One chain for every degree (CGP_RELU_CHAIN): the wave's polynomial (degree 7-13, the
+// shortest whose interval holds every active lane's pixels, kReluChainX) runs as the tail
+// of ONE unrolled degree-13 Horner chain entered at step 14 - d.  Row r (degree 7 + r) of
+// the quartered table holds the top coefficient at [0] and a_(13-j) at [j] for the steps it
+// runs (relu_poly.h), so every row is read at the same SGPR positions.  One chain per ReLU
+// site instead of one per polynomial: the adaptive choice stops growing the code.
+#ifndef CGP_RELU_CHAIN
+#define CGP_RELU_CHAIN 0
+#endif
+constexpr int kChainRows = 7;
+static_assert(sizeof(kReluChainP) == kChainRows * 14 * sizeof(double), "chain table shape");
+struct ChainCoef {
+    double c[kChainRows][14];
+};
+constexpr ChainCoef chain_coef() {
+    ChainCoef t{};
+    for (int r = 0; r < kChainRows; ++r)
+        for (int j = 0; j < 14; ++j) {
+            const int k = j == 0 ? 7 + r : 13 - j;   // the power this entry multiplies
+            double v = kReluChainP[r][j] * 0.0625;
+            for (int n = 0; n < k; ++n) v *= 0.25;
+            t.c[r][j] = v;
+        }
+    return t;
+}
+static __constant__ ChainCoef kReluChainTab = chain_coef();
+
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
     ConstD d, dq;
 #if CGP_RELU_ADAPT
     ConstD a0, a1, a2;
 #endif
+#if CGP_RELU_CHAIN
+    ConstD ch;
+#endif
 };
 __device__ __forceinline__ PolyTab poly_table() {
     ConstD p = (ConstD)kReluPolyTabD.c;
     ConstD q = (ConstD)kReluPolyTabDq.c;
     asm volatile("" : "+s"(p), "+s"(q));
-#if CGP_RELU_ADAPT
+#if CGP_RELU_ADAPT && CGP_RELU_CHAIN
+    ConstD a0 = (ConstD)kReluAdaptTab0.c;
+    ConstD a1 = (ConstD)kReluAdaptTab1.c;
+    ConstD a2 = (ConstD)kReluAdaptTab2.c;
+    ConstD ch = (ConstD)&kReluChainTab.c[0][0];
+    asm volatile("" : "+s"(ch));
+    return PolyTab{p, q, a0, a1, a2, ch};
+#elif CGP_RELU_ADAPT
     ConstD a0 = (ConstD)kReluAdaptTab0.c;
     ConstD a1 = (ConstD)kReluAdaptTab1.c;
     ConstD a2 = (ConstD)kReluAdaptTab2.c;
@@ -336,6 +373,40 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
         for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
 }
+#if CGP_RELU_CHAIN
+// degree d (7..13, wave-uniform) of the one-chain table row t: the first step
+// p = a_d·x4 + a_(d-1) reads its addend at t[14 - d] (a scalar load at a uniform offset), so
+// every degree starts at the same instruction and no per-pixel copy of a_d is needed; steps
+// 15 - d .. 13 follow, 2..7 under uniform branches on d, 8..13 always
+template <int R>
+__device__ __forceinline__ void horner_chain(double (&p)[R], const double (&u)[R], ConstD t,
+                                             int d) {
+    double ck[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) ck[j] = t[j];
+    const double c1 = t[14 - d];
+#pragma unroll
+    for (int r = 0; r < R; ++r) p[r] = fma_sc(ck[0], u[r], c1);
+#pragma unroll
+    for (int j = 2; j <= 13; ++j) {
+        if (j >= 8 || d >= 15 - j) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck[j]);
+        }
+    }
+}
+// the wave's degree: the shortest whose interval holds every active lane's largest x4 (um);
+// a binary search of wave votes (three per ReLU site)
+__device__ __forceinline__ int chain_degree(double um) {
+    auto all = [&](int r) { return __all(um <= 4.0 * kReluChainX[r]); };
+    if (all(3)) {                        // x <= X(10)
+        if (all(1)) return all(0) ? 7 : 8;
+        return all(2) ? 9 : 10;
+    }
+    if (all(5)) return all(4) ? 11 : 12;
+    return 13;
+}
+#endif
 // AD: 0 the full polynomial; 1 the range-adaptive choice, uniform over the wave (its lanes
 // hold one pair); 2 the choice per pair segment: `seg` is the mask of this wave's lanes that
 // hold the same pair as this lane (multi-pair stages, CGP_RELU_ADAPT_MP), so a pair's
@@ -387,6 +458,11 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
+#if CGP_RELU_CHAIN
+        static_assert(kReluPolyDegD == 13, "the one chain is the degree-13 polynomial's");
+        const int d = chain_degree(um);
+        horner_chain<R>(p, u, tab.ch + (d - 7) * 14, d);
+#else
         if (__all(um <= 4.0 * kReluAdaptX0)) {
             horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
         } else if (__all(um <= 4.0 * kReluAdaptX1)) {
@@ -396,6 +472,7 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         } else {
             horner_q<R, kReluPolyDegD>(p, u, tab.dq);
         }
+#endif
     } else {
         horner_q<R, kReluPolyDegD>(p, u, tab.dq);
     }

@@ -206,6 +206,21 @@ __device__ __forceinline__ int opaque_tid() {
 #endif
 }
 
+// An LDS element index folded into one register: ds_read2_b64's offsets reach 255 doubles
+// (2040 bytes), so a window whose constant base (the slot origin) lies further out gets one
+// v_add per read pair; with the base added into the index once, behind an empty asm the
+// compiler cannot see through, the window's reads keep their small immediates
+// (CGP_NET_LDS_BASE, A/B option)
+#ifndef CGP_NET_LDS_BASE
+#define CGP_NET_LDS_BASE 0
+#endif
+__device__ __forceinline__ int lds_index(int e) {
+#if CGP_NET_LDS_BASE
+    asm("" : "+v"(e));
+#endif
+    return e;
+}
+
 // a / d for a >= 0 as an unsigned division (a constant d costs a mul-hi and a shift; the
 // signed form needs three more fix-up ops)
 __device__ __forceinline__ int udiv(int a, int d) { return (int)((unsigned)a / (unsigned)d); }
@@ -434,12 +449,17 @@ __device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, u
 // G::NP pairs: item it of a pass belongs to pair q = it / (items per pair) and works on
 // that pair's LDS arena (q · lds_elems) and variance maps.
 // Range-adaptive ReLU in a conv epilogue: one-pair code votes over the wave (AD 1);
-// multi-pair stages vote per pair segment of the wave (AD 2) with CGP_RELU_ADAPT_MP.
+// multi-pair stages vote per pair segment of the wave (AD 2; CGP_RELU_ADAPT_MP, default on
+// since round 3: +0.5% mnist_as_tf, +0.8% cifar10, profiles/r3/ab_r3k_chain_undef_ldsb_mp.log;
+// =0 keeps the full polynomial there).
 #ifndef CGP_RELU_ADAPT_MP
-#define CGP_RELU_ADAPT_MP 0
+#define CGP_RELU_ADAPT_MP 1
 #endif
 template <int NP>
 constexpr int kAdaptOf = NP == 1 ? 1 : (CGP_RELU_ADAPT_MP ? 2 : 0);
+#ifndef CGP_NET_RES_UNDEF
+#define CGP_NET_RES_UNDEF 0
+#endif
 // lanes of this wave whose item belongs to the same pair as item `it` (items of pair q
 // are [q·per, (q+1)·per); item it sits on lane it % 64 of its wave)
 __device__ __forceinline__ unsigned long long pair_lanes(int it, int per) {
@@ -581,6 +601,14 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         };
         const bool hazard = hits(op.dst) || (DU && hits(op.dst2));
         T res[G::KV][G::R3];
+#if CGP_NET_RES_UNDEF
+        // items past NVT never read res: an empty asm defines it without an instruction
+        // (left undefined, the compiler zeroes every entry on that path: R3 moves per op)
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv)
+#pragma unroll
+            for (int k = 0; k < G::R3; ++k) asm("" : "=v"(res[kv][k]));
+#endif
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * G::NT;
@@ -662,8 +690,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NHT % G::NT == 0 || it < NHT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NH), l = it - q * G::NH;
                 const int qi = udiv(l, G::NG2), g2 = l - qi * G::NG2;
-                const T* row = src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
-                               g2 * G::R2 * G::S + G::OFF;
+                const T* row = lds + lds_index(op.src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
+                                               g2 * G::R2 * G::S + G::OFF);
                 T win[G::WIN2];
 #pragma unroll
                 for (int t = 0; t < G::WIN2; ++t) win[t] = row[t];
@@ -697,7 +725,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
-                const T* col = hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
+                const T* col = lds + lds_index(p.hs + q * arena + g3 * G::R3 * G::S * G::WO + c);
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
