@@ -2,8 +2,9 @@
 
 Workload (BASELINE.json configs[1]): mnist_paper_convnet_gp, Kxx of N = 4096 synthetic
 28×28×1 images, float64, Gram tiles of B = 1024 in the reference's schedule (upper
-triangular tiles).  One STEP = every Gram tile of this rank evaluated into a
-device-resident Kxx.
+triangular tiles).  One STEP = one Gram build: every image's variance maps computed
+once (cnn_gp.gram.ModelKern.bind; the reference recomputes them per tile and side), then
+every Gram tile of this rank evaluated in place into a device-resident Kxx.
 
     python bench.py [--gpus N --steps K --warmup W] [--config C --n N --tile B]
 
@@ -55,6 +56,7 @@ import torch.distributed as dist  # noqa: E402
 import cnn_gp  # noqa: E402
 from cnn_gp import _native as N  # noqa: E402
 from cnn_gp.data import tile_schedule  # noqa: E402
+from cnn_gp.gram import model_kern  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
 FP64_PEAK_TFLOPS = 78.6        # MI355X spec FP64 (vector = matrix); half the FP32 157.3
@@ -404,12 +406,21 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     ref_sched = sum(min(B, n_total - i * B) * min(B, n_total - j * B) for _, i, j in all_tiles)
     K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
 
+    mk = model_kern(model)
+
     def step():
+        # one Gram build: every image's variance maps once (ModelKern.bind), then each
+        # tile from slices of them, written in place into K (cnn_gp.gram's builders)
+        bound = mk.bind(X)
         with torch.no_grad():
             for same, i, j in tiles:
+                a, b = min(B, n_total - i * B), min(B, n_total - j * B)
+                view = K[i * B:i * B + a, j * B:j * B + b]
+                if bound is not None:
+                    bound.tile((same, i * B, j * B, a, b), view)
+                    continue
                 xi = X[i * B:(i + 1) * B]
-                k = model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False)
-                K[i * B:i * B + k.shape[0], j * B:j * B + k.shape[1]].copy_(k)
+                view.copy_(model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False))
 
     for _ in range(warmup):
         step()

@@ -33,7 +33,7 @@ import torch.distributed as dist
 
 from .data import _ceil_div, _tile_order, tile_schedule
 
-__all__ = ("gram_tiles", "gram_local", "gather_gram", "gram_matrix", "model_kern",
+__all__ = ("gram_tiles", "gram_local", "gather_gram", "gram_matrix", "model_kern", "ModelKern",
            "tile_plan", "tile_cost")
 
 Tile = Tuple[bool, int, int, int, int]       # (same, i0, j0, rows, cols)
@@ -56,16 +56,93 @@ def _default_device(device):
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def model_kern(model, device=None, dtype=None) -> Callable:
-    """kern(x, x2, same) -> device tensor: the model evaluated on the device."""
-    def kern(x, x2, same):
-        dev = _default_device(device)
-        xd = x.to(dev, dtype or x.dtype)
+class ModelKern:
+    """kern(x, x2, same) -> device tensor: the model evaluated on the device, one forward
+    per tile (the reference's call, save_kernel.py → kernel_save_tools.py:36-45).
+
+    ``bind(X, X2)`` is the whole-build form the builders below take when they are given a
+    ModelKern: every image's variance maps are computed once for the build
+    (NNGPKernel.image_variances) instead of once per tile and side, and each tile is
+    written straight into its place in the output (NNGPKernel.tile_from_variances).  The
+    maps live as long as the bound object, i.e. one build."""
+
+    def __init__(self, model, device=None, dtype=None):
+        self.model, self.device, self.dtype = model, device, dtype
+
+    def __call__(self, x, x2, same):
+        dev = _default_device(self.device)
+        xd = x.to(dev, self.dtype or x.dtype)
         with torch.no_grad():
             if same:
-                return model(xd)
-            return model(xd, x2.to(dev, dtype or x2.dtype), False, False)
-    return kern
+                return self.model(xd)
+            return self.model(xd, x2.to(dev, self.dtype or x2.dtype), False, False)
+
+    def bind(self, X, X2=None) -> Optional["BoundKern"]:
+        """The build's variance maps of X (and X2), or None when the model has no
+        whole-network program for them (the builders then call the kern per tile)."""
+        if not hasattr(self.model, "image_variances"):
+            return None
+        dev = _default_device(self.device)
+
+        def images(S):
+            if isinstance(S, torch.Tensor):
+                t = S
+            elif hasattr(S, "tensors"):
+                t = S.tensors[0]
+            else:
+                return None
+            return t.to(dev, self.dtype or t.dtype).contiguous()
+        xd = images(X)
+        if xd is None:
+            return None
+        with torch.no_grad():
+            vx = self.model.image_variances(xd)
+            if vx is None:
+                return None
+            if X2 is None:
+                return BoundKern(self.model, vx, vx)
+            yd = images(X2)
+            vy = None if yd is None else self.model.image_variances(yd.to(xd.dtype))
+        return None if vy is None else BoundKern(self.model, vx, vy)
+
+
+class BoundKern:
+    """ModelKern.bind's result: tiles of one build from its precomputed variance maps."""
+
+    def __init__(self, model, vx, vy):
+        self.model, self.vx, self.vy = model, vx, vy
+
+    def tile(self, t: Tile, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Tile t = (same, i0, j0, rows, cols); written into ``out`` when it is a
+        row-major view of the images' dtype, else returned (and copied by the caller)."""
+        same, i0, j0, a, b = t
+        direct = out is not None and out.dtype == self.vx.images.dtype and \
+            out.device == self.vx.images.device and out.dim() == 2 and \
+            out.stride(1) == 1 and tuple(out.shape) == (a, b)
+        with torch.no_grad():
+            k = self.model.tile_from_variances(self.vx, i0, i0 + a, self.vx if same else self.vy,
+                                               j0, j0 + b, same, out=out if direct else None)
+        if out is not None and not direct:
+            out.copy_(k)
+        return k
+
+
+def model_kern(model, device=None, dtype=None) -> ModelKern:
+    """kern(x, x2, same) -> device tensor: the model evaluated on the device (a ModelKern:
+    the builders below evaluate its tiles from one build's variance maps)."""
+    return ModelKern(model, device, dtype)
+
+
+def _fill_tiles(kern, X, src2, X2, tiles, view):
+    """Evaluate ``tiles`` into view(t) (a [rows, cols] slice of the output each): from one
+    bound build when kern is a ModelKern with a whole-network program, else one kern call
+    per tile copied into place."""
+    bound = kern.bind(X, X2) if isinstance(kern, ModelKern) else None
+    for t in tiles:
+        if bound is not None:
+            bound.tile(t, view(t))
+        else:
+            view(t).copy_(_eval_tile(kern, X, src2, t))
 
 
 def tile_cost(t: Tile) -> int:
@@ -128,9 +205,7 @@ def gram_tiles(kern: Callable, X, X2=None, batch_size: int = 1024, worker_rank: 
     if out is None:
         out = torch.full((N, N2), float("nan"), dtype=dtype, device=_default_device(device))
     done = tile_plan(N, None if X2 is None else N2, batch_size, worker_rank, n_workers, split)
-    for t in done:
-        _, i0, j0, a, b = t
-        out[i0:i0 + a, j0:j0 + b].copy_(_eval_tile(kern, X, src2, t))
+    _fill_tiles(kern, X, src2, X2, done, lambda t: out[t[1]:t[1] + t[3], t[2]:t[2] + t[4]])
     return out, done
 
 
@@ -148,11 +223,12 @@ def gram_local(kern: Callable, X, X2=None, batch_size: int = 1024, rank: int = 0
     if cap < need:
         raise ValueError(f"capacity {cap} < {need} elements of rank {rank}'s tiles")
     buf = torch.empty(max(cap, 1), dtype=dtype, device=_default_device(device))
-    off = 0
+    offs, off = {}, 0
     for t in tiles:
-        _, _, _, a, b = t
-        buf[off:off + a * b].view(a, b).copy_(_eval_tile(kern, X, src2, t))
-        off += a * b
+        offs[t] = off
+        off += t[3] * t[4]
+    _fill_tiles(kern, X, src2, X2, tiles,
+                lambda t: buf[offs[t]:offs[t] + t[3] * t[4]].view(t[3], t[4]))
     return buf, tiles
 
 
@@ -341,9 +417,8 @@ def gram_strip(kern: Callable, X, X2=None, batch_size: int = 4096,
     if tuple(out.shape) != (r1 - r0, n2):
         raise ValueError(f"out {tuple(out.shape)} for strip rows {rows} of width {n2}")
     tiles = strip_tiles(N, N2, rows, batch_size)
-    for t in tiles:
-        _, i0, j0, a, b = t
-        out[i0 - r0:i0 - r0 + a, j0:j0 + b].copy_(_eval_tile(kern, X, src2, t))
+    _fill_tiles(kern, X, src2, X2, tiles,
+                lambda t: out[t[1] - r0:t[1] - r0 + t[3], t[2]:t[2] + t[4]])
     return out, tiles, sum(tile_cost(t) for t in tiles)
 
 

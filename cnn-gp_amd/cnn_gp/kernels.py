@@ -8,6 +8,7 @@ storage only: no torch compute runs on the pair maps.
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -31,6 +32,20 @@ def _to_device(t: torch.Tensor, device) -> torch.Tensor:
     if t.device != device:
         t = t.to(device, non_blocking=True)
     return t.contiguous()
+
+
+class _ImageVariances:
+    """Variance maps of one image set for one Gram build (NNGPKernel.image_variances):
+    var[v] = [N, h, w] maps of every value the whole-network kernel reads, qvar[v] their
+    quartered x-side copies (fp64 closed-form ReLU), key = (H, W, dtype, plan flags)."""
+
+    __slots__ = ("images", "var", "qvar", "key")
+
+    def __init__(self, images, var, qvar, key):
+        self.images, self.var, self.qvar, self.key = images, var, qvar, key
+
+    def __len__(self):
+        return len(self.images)
 
 
 class NNGPKernel(nn.Module):
@@ -165,6 +180,63 @@ class NNGPKernel(nn.Module):
             raise RuntimeError(f"the model's output is {plan.final_hw[0]}x{plan.final_hw[1]}"
                                " per pair, not 1x1: add a final Conv2d covering the map")
         return out.view(n1) if diag else out.view(n1, n2)
+
+    # ---- Gram builds: every image's variance maps once per build -------------------
+    # The reference (and forward above) recomputes the per-image variance recursion
+    # (kernels.py:44-49, then every layer on the same/diag path) for both image blocks of
+    # every tile: a Gram build over B-row tiles of N images does it about 2N/B times per
+    # image.  image_variances() runs the whole-network program's variance chain once over
+    # an image set; tile_from_variances() evaluates one tile from slices of two such sets.
+    # Nothing is kept between builds (the caller holds the maps for one build).
+
+    def image_variances(self, x: torch.Tensor):
+        """The variance maps every whole-network tile of images ``x`` ([N, C, H, W], on the
+        device) reads, computed in one launch: an object for tile_from_variances, or None
+        when the model runs on the layer path (shapes netfuse lacks, CGP_VAR_CHAIN=0, maps
+        the chain kernel cannot hold) -- callers then fall back to forward()."""
+        if x.device.type != "cuda" or x.dtype not in (torch.float32, torch.float64) or \
+                x.dim() != 4 or not VAR_CHAIN:
+            return None
+        n, _, h, w = x.shape
+        plan = self._plan(h, w)
+        net = self._net_plan(plan, x.element_size())
+        if net is None:
+            return None
+        x = x.contiguous()
+        with torch.cuda.device(x.device):
+            fused = plan.run_variances_fused(x, x, n, n, True, _stream_handle(x.device),
+                                             net.need_var,
+                                             net.quarter_vars(x.dtype, plan.flags))
+        if fused is None:
+            return None
+        var, qvar = fused
+        return _ImageVariances(x, {v: xx for v, (xx, _) in var.items()}, dict(qvar),
+                               (h, w, x.dtype, plan.flags))
+
+    def tile_from_variances(self, vx: "_ImageVariances", i0: int, i1: int,
+                            vy: "_ImageVariances", j0: int, j1: int, same: bool,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """K[i0:i1, j0:j1] of vx's images against vy's, equal to
+        forward(vx.images[i0:i1], vy.images[j0:j1], same, False) (same: a diagonal tile,
+        the same rows of one set).  ``out``: an [i1 - i0, j1 - j0] row-major view of the
+        images' dtype to write into (e.g. a tile of the Gram matrix)."""
+        if vx.key != vy.key:
+            raise ValueError("tile_from_variances: the two image sets were prepared for "
+                             "different shapes, dtypes or ReLU modes")
+        if same and (vx is not vy or (i0, i1) != (j0, j1)):
+            raise ValueError("a diagonal tile takes the same rows of one image set")
+        h, w, dtype, flags = vx.key
+        plan = self._plan(h, w)
+        if plan.flags != flags:
+            raise ValueError("tile_from_variances: the model's ReLU mode changed since "
+                             "image_variances")
+        net = self._net_plan(plan, torch.empty((), dtype=dtype).element_size())
+        x, y = vx.images[i0:i1], vy.images[j0:j1]
+        var = {v: (m[i0:i1], vy.var[v][j0:j1]) for v, m in vx.var.items()}
+        qvar = {v: q[i0:i1] for v, q in vx.qvar.items()}
+        with torch.cuda.device(x.device):
+            return net.run(x, y, var, i1 - i0, j1 - j0, same, _stream_handle(x.device),
+                           flags, out=out, qvar=qvar or None)
 
     def layers(self):
         return 0

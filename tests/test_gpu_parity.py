@@ -844,3 +844,64 @@ def test_var_chain_rejects_maps_grown_by_padding():
         got = m(x.to(DEV), y.to(DEV), False, False).cpu().numpy()
     ref = O.kernel(spec, x.numpy(), y.numpy(), False, False)
     assert rel_err(got, ref) < RTOL64["fast"]
+
+
+# ------------------------------------------------------------------------------------
+# Gram builds from one build's variance maps (ModelKern.bind) == one forward per tile
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp",
+                                 "mnist_as_tf", "cifar10"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_bound_build_bit_equal_to_per_tile_forward(cfg, dtype):
+    """gram_tiles / gram_strip with a ModelKern compute every image's variance maps once
+    and write each tile in place; the result must be bit-equal to the reference's call
+    pattern (one model forward per tile, copied into place) — Kxx with ragged edge tiles,
+    Kxz, and a strip that starts mid-matrix."""
+    from cnn_gp import gram
+    m = configs_util.model(cfg).to(DEV, dtype)
+    C = 3 if cfg == "cifar10" else 1
+    side = 32 if C == 3 else 28
+    g = torch.Generator().manual_seed(11)
+    X = torch.rand((300, C, side, side), generator=g, dtype=dtype).to(DEV)
+    Z = torch.rand((130, C, side, side), generator=g, dtype=dtype).to(DEV)
+    mk = gram.model_kern(m)
+    assert mk.bind(X) is not None
+
+    def per_tile(x, x2, same):          # a plain callable: the builders' per-tile path
+        return mk(x, x2, same)
+
+    for X2 in (None, Z):
+        a, _ = gram.gram_tiles(mk, X, X2, 128, dtype=dtype)
+        b, _ = gram.gram_tiles(per_tile, X, X2, 128, dtype=dtype)
+        assert torch.equal(torch.isnan(a), torch.isnan(b))
+        assert torch.equal(a[~torch.isnan(a)], b[~torch.isnan(b)]), (cfg, dtype, X2 is None)
+    s1, _, p1 = gram.gram_strip(mk, X, None, 128, (72, 200), dtype=dtype)
+    s2, _, p2 = gram.gram_strip(per_tile, X, None, 128, (72, 200), dtype=dtype)
+    assert p1 == p2
+    assert torch.equal(torch.isnan(s1), torch.isnan(s2))
+    assert torch.equal(s1[~torch.isnan(s1)], s2[~torch.isnan(s2)])
+
+
+def test_bound_build_exact_relu_and_checks():
+    """the op-by-op ReLU (no quartered maps) through the bound path, the float64 matrix of
+    a float32 model (tiles copied, not written in place), and the argument checks"""
+    from cnn_gp import gram
+    m = configs_util.model("mnist_as_tf").to(DEV, torch.float64).set_exact_relu(True)
+    g = torch.Generator().manual_seed(12)
+    X = torch.rand((150, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    mk = gram.model_kern(m)
+    a, _ = gram.gram_tiles(mk, X, None, 64)
+    b, _ = gram.gram_tiles(lambda x, x2, same: mk(x, x2, same), X, None, 64)
+    assert torch.equal(a[~torch.isnan(a)], b[~torch.isnan(b)])
+    m32 = configs_util.model("mnist_paper_convnet_gp").to(DEV, torch.float32)
+    X32 = X.float()
+    c, _ = gram.gram_tiles(gram.model_kern(m32), X32, None, 64, dtype=torch.float64)
+    ref = m32(X32).double()
+    iu = torch.triu_indices(150, 150)
+    assert torch.equal(c[iu[0], iu[1]], ref[iu[0], iu[1]])
+    vx = m.image_variances(X)
+    v32 = m32.image_variances(X32)
+    with pytest.raises(ValueError):
+        m.tile_from_variances(vx, 0, 10, v32, 0, 10, False)
+    with pytest.raises(ValueError):
+        m.tile_from_variances(vx, 0, 10, vx, 10, 20, True)
