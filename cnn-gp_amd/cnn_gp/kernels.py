@@ -189,11 +189,13 @@ class NNGPKernel(nn.Module):
     # an image set; tile_from_variances() evaluates one tile from slices of two such sets.
     # Nothing is kept between builds (the caller holds the maps for one build).
 
-    def image_variances(self, x: torch.Tensor):
+    def image_variances(self, x: torch.Tensor, max_bytes: Optional[int] = None):
         """The variance maps every whole-network tile of images ``x`` ([N, C, H, W], on the
         device) reads, computed in one launch: an object for tile_from_variances, or None
         when the model runs on the layer path (shapes netfuse lacks, CGP_VAR_CHAIN=0, maps
-        the chain kernel cannot hold) -- callers then fall back to forward()."""
+        the chain kernel cannot hold) or the maps would take more than ``max_bytes``
+        (default: a quarter of the device's free memory) -- callers then fall back to
+        forward() per tile."""
         if x.device.type != "cuda" or x.dtype not in (torch.float32, torch.float64) or \
                 x.dim() != 4 or not VAR_CHAIN:
             return None
@@ -202,11 +204,19 @@ class NNGPKernel(nn.Module):
         net = self._net_plan(plan, x.element_size())
         if net is None:
             return None
+        quarter = net.quarter_vars(x.dtype, plan.flags)
+        chain = plan._var_chain(set(net.need_var), set(quarter) & set(net.need_var), x.device)
+        if chain is None:
+            return None
+        size = n * (chain["total"] + chain["qtotal"]) * x.element_size()
+        if max_bytes is None:
+            max_bytes = torch.cuda.mem_get_info(x.device)[0] // 4
+        if size > max_bytes:
+            return None
         x = x.contiguous()
         with torch.cuda.device(x.device):
             fused = plan.run_variances_fused(x, x, n, n, True, _stream_handle(x.device),
-                                             net.need_var,
-                                             net.quarter_vars(x.dtype, plan.flags))
+                                             net.need_var, quarter)
         if fused is None:
             return None
         var, qvar = fused

@@ -905,3 +905,5 @@ def test_bound_build_exact_relu_and_checks():
         m.tile_from_variances(vx, 0, 10, v32, 0, 10, False)
     with pytest.raises(ValueError):
         m.tile_from_variances(vx, 0, 10, vx, 10, 20, True)
+    # maps larger than the caller's budget: no bound build (the builders go per tile)
+    assert m.image_variances(X, max_bytes=1024) is None
