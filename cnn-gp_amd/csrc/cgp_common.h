@@ -209,17 +209,26 @@ static __constant__ AdaptCoef<kReluAdaptDeg0> kReluAdaptTab0 = adapt_coef<kReluA
 static __constant__ AdaptCoef<kReluAdaptDeg1> kReluAdaptTab1 = adapt_coef<kReluAdaptDeg1>(kReluAdaptP1);
 static __constant__ AdaptCoef<kReluAdaptDeg2> kReluAdaptTab2 = adapt_coef<kReluAdaptDeg2>(kReluAdaptP2);
 
-// One chain for every degree (CGP_RELU_CHAIN): the wave's polynomial (degree 7-13, the
-// shortest whose interval holds every active lane's pixels, kReluChainX) runs as the tail
-// of ONE unrolled degree-13 Horner chain entered at step 14 - d.  Row r (degree 7 + r) of
-// the quartered table holds the top coefficient at [0] and a_(13-j) at [j] for the steps it
-// runs (relu_poly.h), so every row is read at the same SGPR positions.  One chain per ReLU
-// site instead of one per polynomial: the adaptive choice stops growing the code.
+// Per-degree polynomials (relu_poly.h kReluChainP: degrees 6-13, each fitted on [0, X_d] at
+// or below the degree-13 bound), all in one row layout: row r = degree d = kReluChainD0 + r
+// holds the top coefficient a_d at [0] and a_(13-j) at [j] for the steps j >= 14 - d it runs,
+// so every degree's Horner steps read the same SGPR positions.  Two ways to run them:
+//  * CGP_RELU_FINE (A/B, off): the wave's degree from a binary search of votes (three per
+//    ReLU site), then that degree's own unrolled chain (one per degree in the code);
+//    −1% VALU instructions, time within ±1% (cifar10 −2%; profiles/r3/ab_r3p_relu_fine.log);
+//  * CGP_RELU_CHAIN (A/B, off): ONE unrolled degree-13 chain entered at step 14 - d; the
+//    code holds one chain per ReLU site (measured: code size is not a cost, and the chain's
+//    coefficient SGPRs add spills).
+#ifndef CGP_RELU_FINE
+#define CGP_RELU_FINE 0
+#endif
 #ifndef CGP_RELU_CHAIN
 #define CGP_RELU_CHAIN 0
 #endif
-constexpr int kChainRows = 7;
+constexpr int kChainD0 = kReluChainD0;
+constexpr int kChainRows = 14 - kChainD0;
 static_assert(sizeof(kReluChainP) == kChainRows * 14 * sizeof(double), "chain table shape");
+static_assert(sizeof(kReluChainX) == (kChainRows - 1) * sizeof(double), "chain thresholds");
 struct ChainCoef {
     double c[kChainRows][14];
 };
@@ -227,7 +236,7 @@ constexpr ChainCoef chain_coef() {
     ChainCoef t{};
     for (int r = 0; r < kChainRows; ++r)
         for (int j = 0; j < 14; ++j) {
-            const int k = j == 0 ? 7 + r : 13 - j;   // the power this entry multiplies
+            const int k = j == 0 ? kChainD0 + r : 13 - j;   // the power this entry multiplies
             double v = kReluChainP[r][j] * 0.0625;
             for (int n = 0; n < k; ++n) v *= 0.25;
             t.c[r][j] = v;
@@ -242,7 +251,7 @@ struct PolyTab {
 #if CGP_RELU_ADAPT
     ConstD a0, a1, a2;
 #endif
-#if CGP_RELU_CHAIN
+#if CGP_RELU_CHAIN || CGP_RELU_FINE
     ConstD ch;
 #endif
 };
@@ -250,12 +259,14 @@ __device__ __forceinline__ PolyTab poly_table() {
     ConstD p = (ConstD)kReluPolyTabD.c;
     ConstD q = (ConstD)kReluPolyTabDq.c;
     asm volatile("" : "+s"(p), "+s"(q));
-#if CGP_RELU_ADAPT && CGP_RELU_CHAIN
+#if CGP_RELU_ADAPT && (CGP_RELU_CHAIN || CGP_RELU_FINE)
     ConstD a0 = (ConstD)kReluAdaptTab0.c;
     ConstD a1 = (ConstD)kReluAdaptTab1.c;
     ConstD a2 = (ConstD)kReluAdaptTab2.c;
     ConstD ch = (ConstD)&kReluChainTab.c[0][0];
-    asm volatile("" : "+s"(ch));
+    // every table pointer opaque: a known address lets the compiler hoist the coefficient
+    // loads out of the pair loop and keep them all in SGPRs (spills)
+    asm volatile("" : "+s"(a0), "+s"(a1), "+s"(a2), "+s"(ch));
     return PolyTab{p, q, a0, a1, a2, ch};
 #elif CGP_RELU_ADAPT
     ConstD a0 = (ConstD)kReluAdaptTab0.c;
@@ -373,11 +384,11 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
         for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
 }
-#if CGP_RELU_CHAIN
-// degree d (7..13, wave-uniform) of the one-chain table row t: the first step
+#if CGP_RELU_CHAIN || CGP_RELU_FINE
+// one-chain form: degree d (wave-uniform) of table row t: the first step
 // p = a_d·x4 + a_(d-1) reads its addend at t[14 - d] (a scalar load at a uniform offset), so
 // every degree starts at the same instruction and no per-pixel copy of a_d is needed; steps
-// 15 - d .. 13 follow, 2..7 under uniform branches on d, 8..13 always
+// 15 - d .. 13 follow, those below 15 - kChainD0 under uniform branches on d
 template <int R>
 __device__ __forceinline__ void horner_chain(double (&p)[R], const double (&u)[R], ConstD t,
                                              int d) {
@@ -389,22 +400,48 @@ __device__ __forceinline__ void horner_chain(double (&p)[R], const double (&u)[R
     for (int r = 0; r < R; ++r) p[r] = fma_sc(ck[0], u[r], c1);
 #pragma unroll
     for (int j = 2; j <= 13; ++j) {
-        if (j >= 8 || d >= 15 - j) {
+        if (j >= 15 - kChainD0 || d >= 15 - j) {
 #pragma unroll
             for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck[j]);
         }
     }
 }
-// the wave's degree: the shortest whose interval holds every active lane's largest x4 (um);
-// a binary search of wave votes (three per ReLU site)
-__device__ __forceinline__ int chain_degree(double um) {
-    auto all = [&](int r) { return __all(um <= 4.0 * kReluChainX[r]); };
-    if (all(3)) {                        // x <= X(10)
-        if (all(1)) return all(0) ? 7 : 8;
-        return all(2) ? 9 : 10;
+// per-degree form: degree D's own chain from its table row (compile-time steps)
+template <int R, int D>
+__device__ __forceinline__ void horner_row(double (&p)[R], const double (&u)[R], ConstD t) {
+    const double top = t[0], c1 = t[14 - D];
+#pragma unroll
+    for (int r = 0; r < R; ++r) p[r] = fma_sc(top, u[r], c1);
+#pragma unroll
+    for (int j = 15 - D; j <= 13; ++j) {
+        const double ck = t[j];
+#pragma unroll
+        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
-    if (all(5)) return all(4) ? 11 : 12;
-    return 13;
+}
+// the wave's degree: the shortest whose interval holds every active lane's largest x4 (um);
+// a binary search of wave votes over kReluChainX (three per ReLU site)
+__device__ __forceinline__ int chain_degree(double um) {
+    static_assert(kChainRows == 8, "the search below covers degrees 6..13");
+    auto all = [&](int r) { return __all(um <= 4.0 * kReluChainX[r]); };
+    if (all(3)) {                                  // x <= X(9)
+        if (all(1)) return all(0) ? 6 : 7;
+        return all(2) ? 8 : 9;
+    }
+    if (all(5)) return all(4) ? 10 : 11;
+    return all(6) ? 12 : 13;
+}
+template <int R, int D = kChainD0>
+__device__ __forceinline__ void horner_pick(double (&p)[R], const double (&u)[R], ConstD tab,
+                                            int d) {
+    if constexpr (D == 13) {
+        horner_row<R, 13>(p, u, tab + (13 - kChainD0) * 14);
+    } else {
+        if (d == D)
+            horner_row<R, D>(p, u, tab + (D - kChainD0) * 14);
+        else
+            horner_pick<R, D + 1>(p, u, tab, d);
+    }
 }
 #endif
 // AD: 0 the full polynomial; 1 the range-adaptive choice, uniform over the wave (its lanes
@@ -458,10 +495,14 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
-#if CGP_RELU_CHAIN
-        static_assert(kReluPolyDegD == 13, "the one chain is the degree-13 polynomial's");
+#if CGP_RELU_CHAIN || CGP_RELU_FINE
+        static_assert(kReluPolyDegD == 13, "the per-degree rows end in the degree-13 polynomial");
         const int d = chain_degree(um);
-        horner_chain<R>(p, u, tab.ch + (d - 7) * 14, d);
+#if CGP_RELU_CHAIN
+        horner_chain<R>(p, u, tab.ch + (d - kChainD0) * 14, d);
+#else
+        horner_pick<R>(p, u, tab.ch, d);
+#endif
 #else
         if (__all(um <= 4.0 * kReluAdaptX0)) {
             horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);

@@ -124,18 +124,21 @@ def test_float_closed_form():
 
 
 def chain_tables():
-    """relu_poly.h's one-chain tables (CGP_RELU_CHAIN): thresholds of degrees 7-12 and the
-    7 x 14 rows (degree 7 + r: a_d at [0], a_(13-j) at [j] for the steps it runs)."""
+    """relu_poly.h's per-degree tables (CGP_RELU_FINE / CGP_RELU_CHAIN): the lowest degree
+    d0, the thresholds of degrees d0..12 and the rows (degree d0 + r: a_d at [0], a_(13-j) at
+    [j] for the steps it runs)."""
     txt = open(HDR).read()
+    d0 = int(re.search(r"kReluChainD0 = (\d+);", txt).group(1))
     xs = re.search(r"kReluChainX\[\d+\] = \{(.*?)\};", txt, re.S).group(1)
-    body = re.search(r"kReluChainP\[7\]\[14\] = \{(.*?)\};", txt, re.S).group(1)
+    body = re.search(r"kReluChainP\[\d+\]\[14\] = \{(.*?)\};", txt, re.S).group(1)
     rows = [[float(v) for v in r.split(",") if v.strip()]
             for r in re.findall(r"\{([^{}]*)\}", body)]
-    return [float(v) for v in xs.split(",")], rows
+    return d0, [float(v) for v in xs.split(",")], rows
 
 
 def chain_eval(row, d, x):
-    """horner_chain (cgp_common.h) in numpy: p = a_d·x + t[14-d], then steps 15-d .. 13."""
+    """horner_row / horner_chain (cgp_common.h) in numpy: p = a_d·x + t[14-d], then steps
+    15-d .. 13."""
     p = row[0] * x + row[14 - d]
     for j in range(15 - d, 14):
         p = p * x + row[j]
@@ -143,19 +146,19 @@ def chain_eval(row, d, x):
 
 
 def test_chain_tables_hold_each_degree_at_the_degree13_bound():
-    xs, rows = chain_tables()
-    assert len(rows) == 7 and all(len(r) == 14 for r in rows)
-    assert xs == sorted(xs) and len(xs) == 6
+    d0, xs, rows = chain_tables()
+    assert len(rows) == 14 - d0 and all(len(r) == 14 for r in rows)
+    assert xs == sorted(xs) and len(xs) == len(rows) - 1
     full = coeffs("D")
-    assert rows[6][0] == full[13] and rows[6][1:] == full[12::-1]
+    assert rows[-1][0] == full[13] and rows[-1][1:] == full[12::-1]
     getcontext().prec = 50
     sys.path.insert(0, os.path.join(os.path.dirname(PKG), "tools"))
     from fit_relu_poly import P_dec
     for r, row in enumerate(rows):
-        d = 7 + r
+        d = d0 + r
         # the entries before the first step of degree d are unused zeros
         assert all(v == 0.0 for v in row[1:14 - d]), d
-        xmax = xs[r] if r < 6 else 0.5
+        xmax = xs[r] if r < len(xs) else 0.5
         x = np.linspace(0.0, xmax, 257)
         got = chain_eval(row, d, x)
         ref = np.array([float(P_dec(Decimal(float(v)))) for v in x])

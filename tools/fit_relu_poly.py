@@ -120,11 +120,11 @@ def check(monox, dt, npts=20001, xmax=0.5):
 ADAPT = ((0.125, 7), (0.25, 9), (0.375, 11))
 # ... and for the float polynomial (its bound: the degree-6 fit's 7.9e-8)
 ADAPT_F = ((0.125, 3), (0.375, 5))
-# one Horner chain for every degree (CGP_RELU_CHAIN): degrees 7-12 on [0, xmax] at or below
-# the degree-13 fit's bound, the degree-13 polynomial itself on [0, 1/2]; the kernel enters
-# one unrolled degree-13 chain at the step of the wave's degree, so the code holds one chain
-# per ReLU site instead of one per polynomial
-CHAIN = ((0.13, 7), (0.19, 8), (0.25, 9), (0.31, 10), (0.375, 11), (0.43, 12))
+# every degree 6-12 on [0, xmax] at or below the degree-13 fit's bound, the degree-13
+# polynomial itself on [0, 1/2], in one table layout (kReluChainP): the fine-grained
+# adaptive ReLU (CGP_RELU_FINE) takes the wave's degree by a binary search of votes, and the
+# one-chain option (CGP_RELU_CHAIN) enters one unrolled degree-13 chain at that degree's step
+CHAIN = ((0.083, 6), (0.13, 7), (0.19, 8), (0.25, 9), (0.31, 10), (0.375, 11), (0.43, 12))
 
 
 def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
@@ -175,9 +175,12 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
                   f"constexpr float kReluAdaptFP{k}[{d + 1}] = {{"]
         lines += [f"    {float(c)!r}f," for c in cfs]
         lines += ["};"]
-    # chain rows: degree 7 + row; entry 0 = the top coefficient a_d, entry j = a_(13-j) for
-    # j >= 14 - d (the steps degree d runs), 0 before that
-    lines += ["// one-chain tables (CGP_RELU_CHAIN): row r = degree 7 + r on x in [0, kReluChainX[r]]"]
+    # chain rows: degree CHAIN[0] + row; entry 0 = the top coefficient a_d, entry j = a_(13-j)
+    # for j >= 14 - d (the steps degree d runs), 0 before that
+    d0 = chain[0][1]
+    lines += [f"// per-degree tables (CGP_RELU_FINE, CGP_RELU_CHAIN): row r = degree {d0} + r on x in "
+              "[0, kReluChainX[r]]",
+              f"constexpr int kReluChainD0 = {d0};"]
     lines += [f"//   degree {d}: x <= {xm}, max rel err {err:.2e}" for xm, d, (err, _) in chain]
     lines += [f"//   degree {deg_d}: x <= 0.5, max rel err {dbl[deg_d][0]:.2e}"]
     lines += [f"constexpr double kReluChainX[{len(chain)}] = {{"
