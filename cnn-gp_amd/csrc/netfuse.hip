@@ -1310,6 +1310,11 @@ constexpr int net_wpe(long long lds_bytes, int cap = 5, int waves = kNT / 64) {
 #ifndef CGP_NET_PROG_WPE_MAX
 #define CGP_NET_PROG_WPE_MAX 5
 #endif
+// register target cap of the multi-pair (4 / 16 pairs) fp64 stage programs (A/B knob: the
+// per-segment adaptive ReLU spills 13 VGPRs in mnist_as_tf's 14x14 stage at 5)
+#ifndef CGP_NET_PROG_WPE_MP
+#define CGP_NET_PROG_WPE_MP CGP_NET_PROG_WPE_MAX
+#endif
 
 // the instantiation for (EX, DU, pairs, LDS footprint of the workgroup): the fp64 closed
 // form — the production path — has a register target per occupancy level; fp32 one per
@@ -1366,7 +1371,9 @@ const void* prog_fn_one() {
         constexpr long long bytes =
             (long long)I.lds_elems * (long long)sizeof(T) * kUnitsOf<I.pairs>;
         constexpr int wpe = sizeof(T) == 8
-                                ? net_wpe(bytes, CGP_NET_PROG_WPE_MAX, kNTof<I.pairs> / 64)
+                                ? net_wpe(bytes, I.pairs > 2 ? CGP_NET_PROG_WPE_MP
+                                                             : CGP_NET_PROG_WPE_MAX,
+                                          kNTof<I.pairs> / 64)
                                 : CGP_NET_PROG_WPE_F32 > 0
                                       ? net_wpe(bytes, CGP_NET_PROG_WPE_F32, kNTof<I.pairs> / 64)
                                       : (I.dual ? 4 : 5);

@@ -101,7 +101,16 @@ def main():
                     ev.append((a._obj.pairs, e0, e1))
                     return rc
             real = N.load
-            N.load = lambda: type("L", (), {f"cgp_net_{sfx}": Timed()})()
+
+            class Wrap:                 # the library with cgp_net_<sfx> timed
+                def __init__(self, lib_):
+                    self._lib = lib_
+                    setattr(self, f"cgp_net_{sfx}", Timed())
+
+                def __getattr__(self, k):
+                    return getattr(self._lib, k)
+            wrapped = Wrap(real())
+            N.load = lambda: wrapped
             try:
                 net.run(X, Z, var, B, B, args.same, sh, plan.flags, out=out)
             finally:
