@@ -235,6 +235,10 @@ class NNGPKernel(nn.Module):
                              "different shapes, dtypes or ReLU modes")
         if same and (vx is not vy or (i0, i1) != (j0, j1)):
             raise ValueError("a diagonal tile takes the same rows of one image set")
+        # the kernel indexes the sliced maps by the tile's extents: they must be in range
+        if not (0 <= i0 < i1 <= len(vx) and 0 <= j0 < j1 <= len(vy)):
+            raise ValueError(f"tile rows [{i0}, {i1}) x cols [{j0}, {j1}) outside the image "
+                             f"sets ({len(vx)}, {len(vy)})")
         h, w, dtype, flags = vx.key
         plan = self._plan(h, w)
         if plan.flags != flags:

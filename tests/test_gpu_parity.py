@@ -905,5 +905,9 @@ def test_bound_build_exact_relu_and_checks():
         m.tile_from_variances(vx, 0, 10, v32, 0, 10, False)
     with pytest.raises(ValueError):
         m.tile_from_variances(vx, 0, 10, vx, 10, 20, True)
+    with pytest.raises(ValueError):               # rows past the image set
+        m.tile_from_variances(vx, 140, 160, vx, 0, 20, False)
+    with pytest.raises(ValueError):
+        m.tile_from_variances(vx, 0, 10, vx, 5, 5, False)
     # maps larger than the caller's budget: no bound build (the builders go per tile)
     assert m.image_variances(X, max_bytes=1024) is None
