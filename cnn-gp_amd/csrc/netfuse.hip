@@ -460,6 +460,38 @@ constexpr int kAdaptOf = NP == 1 ? 1 : (CGP_RELU_ADAPT_MP ? 2 : 0);
 #ifndef CGP_NET_RES_UNDEF
 #define CGP_NET_RES_UNDEF 0
 #endif
+// Wave priority (CGP_NET_PRIO, default 2): a conv raises its waves' issue priority
+// (s_setprio) while it sends its variance loads and window reads and drops it for the
+// arithmetic epilogue, so the memory requests of a wave entering an op go out ahead of the
+// other waves' long ALU runs and their latency overlaps that work.  Measured (one B = 1024
+// Kxz tile, profiles/r3/ab_r3u_prio.log): ConvNet +4.5-5%, Residual +4-5%, mnist_as_tf +3%
+// (its 28x28 head; the multi-pair stages do not move), but the cifar10 head (32x32 maps,
+// four waves per SIMD) -3%: applied to maps of at most CGP_NET_PRIO_MAXHW pixels.
+#ifndef CGP_NET_PRIO
+#define CGP_NET_PRIO 2
+#endif
+#ifndef CGP_NET_PRIO_MP      // also in the multi-pair (4 / 16 pairs) stages
+#define CGP_NET_PRIO_MP 1
+#endif
+#ifndef CGP_NET_PRIO_MAXHW
+#define CGP_NET_PRIO_MAXHW (28 * 28)
+#endif
+template <int NP, int HW>
+constexpr bool kPrioOn = CGP_NET_PRIO > 0 && (NP == 1 || CGP_NET_PRIO_MP) &&
+                         HW <= CGP_NET_PRIO_MAXHW;
+template <int NP, int HW>
+__device__ __forceinline__ void prio_mem() {
+    if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(CGP_NET_PRIO);
+}
+template <int NP, int HW>
+__device__ __forceinline__ void prio_alu() {
+    if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(0);
+}
+// the same around the loads of the elementwise ops (moments, standalone ReLU, LINEAR):
+// A/B option CGP_NET_PRIO_ELEM
+#ifndef CGP_NET_PRIO_ELEM
+#define CGP_NET_PRIO_ELEM 0
+#endif
 // lanes of this wave whose item belongs to the same pair as item `it` (items of pair q
 // are [q·per, (q+1)·per); item it sits on lane it % 64 of its wave)
 __device__ __forceinline__ unsigned long long pair_lanes(int it, int per) {
@@ -480,6 +512,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
+    prio_mem<NP, G::HW>();
     const VarSrc<T> vs0 = var_src<T, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
         if constexpr (NP == 1) {
@@ -494,6 +527,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const int wsi = op.ws_in, wso = op.ws_out;
 
     if constexpr (G::REDUCE && NP == 1) {
+        prio_alu<NP, G::HW>();
         // 1x1 output from a full-plane window: a block reduction
         T acc = T(0);
 #pragma unroll
@@ -523,6 +557,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::REDUCE) {
+        prio_alu<NP, G::HW>();
         // NP pairs: G::NT / NP lanes per pair (within one wave) sum its map, then a
         // segmented butterfly; the group's first lane finishes the pair
         constexpr int TPP = G::NT / NP;
@@ -553,6 +588,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             net_out<T, EX, DU, 1>(lds, op, v, at, ok, u1, u2, tab);
         }
     } else if constexpr (G::POINT) {
+        prio_alu<NP, G::HW>();
         constexpr int N = NP * G::HOWO;
         constexpr int KP = (N + G::NT - 1) / G::NT;
         T u1[KP], u2[KP], v[KP];
@@ -638,6 +674,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
             }
         }
+        prio_alu<NP, G::HW>();
         if (hazard) lds_barrier();
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
@@ -736,6 +773,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 for (int k = 0; k < G::R3; ++k) asm volatile("" : "+v"(u1[kv][k]), "+v"(u2[kv][k]));
                 T o[G::R3], v[G::R3];
                 win_sums<T, G::TAPS, G::S, G::R3>(win, o);
+                prio_alu<NP, G::HW>();
                 int at[G::R3];
                 bool ok[G::R3];
 #pragma unroll
@@ -781,6 +819,8 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     const int n = NP * hw;
     // waves with no pixel in this pass skip the ReLUs (uniform per wave)
     const bool live = base + (tid & ~63) < n;
+    constexpr bool kPE = CGP_NET_PRIO_ELEM && kPrioOn<NP, (W_ > 0 ? W_ * W_ : 0)>;
+    if constexpr (kPE) prio_mem<NP, 0>();
     T a[KE], u1[KE], u2[KE];
     int at[KE];
     bool ok[KE];
@@ -814,6 +854,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
         }
     }
+    if constexpr (kPE) prio_alu<NP, 0>();
     if constexpr (KIND == CGP_NET_MOMENTS) {
         // the channel mean (x / 1 == x: a uniform branch, so one-channel inputs run no
         // division at all)
