@@ -487,6 +487,21 @@ template <int NP, int HW>
 __device__ __forceinline__ void prio_alu() {
     if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(0);
 }
+// CGP_NET_PRIO_SPAN (A/B): 0 = the variance loads and the window reads (default), 1 = the
+// variance loads only (dropped before the window reads: loses most of the gain), 2 = the
+// window reads only (raised after the variance loads)
+#ifndef CGP_NET_PRIO_SPAN
+#define CGP_NET_PRIO_SPAN 0
+#endif
+template <int NP, int HW>
+__device__ __forceinline__ void prio_before_loads() {
+    if constexpr (CGP_NET_PRIO_SPAN != 2) prio_mem<NP, HW>();
+}
+template <int NP, int HW>
+__device__ __forceinline__ void prio_after_loads() {
+    if constexpr (CGP_NET_PRIO_SPAN == 1) prio_alu<NP, HW>();
+    if constexpr (CGP_NET_PRIO_SPAN == 2) prio_mem<NP, HW>();
+}
 // the same around the loads of the elementwise ops (moments, standalone ReLU, LINEAR):
 // A/B option CGP_NET_PRIO_ELEM
 #ifndef CGP_NET_PRIO_ELEM
@@ -512,7 +527,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
-    prio_mem<NP, G::HW>();
+    prio_before_loads<NP, G::HW>();
     const VarSrc<T> vs0 = var_src<T, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
         if constexpr (NP == 1) {
@@ -629,6 +644,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 u2[kv][k] = vs.on ? vs.ldy(px0, k * G::WO) : T(1);
             }
         }
+        prio_after_loads<NP, G::HW>();
         // outputs that land on the source (in place, or dst2 on the source) are stored
         // after every item has read its window
         const int s_lo = op.src - wsi, s_hi = op.src + G::H * wsi;
@@ -720,6 +736,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) u1[kv][k] = u2[kv][k] = T(1);
         }
+        prio_after_loads<NP, G::HW>();
         // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
 #pragma unroll
         for (int kh = 0; kh < G::KH; ++kh) {
