@@ -8,19 +8,28 @@ every Gram tile of this rank evaluated in place into a device-resident Kxx.
 
     python bench.py [--gpus N --steps K --warmup W] [--config C --n N --tile B]
 
+--gpus N > 1 without a torchrun environment: this process does no GPU work, starts
+``python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>`` as a
+child (one rank per GPU, RCCL over xGMI — the reference's run.bash:14-36 starts one
+save_kernel.py per visible GPU the same way) and exits with its status.  Under torchrun
+--gpus must equal WORLD_SIZE.  CGP_BENCH_BACKEND=gloo rehearses the multi-rank path with
+ranks sharing the GPUs there are.
+
 value = kernel entries the device EVALUATES per second, whole job: B1·B2 for an
 off-diagonal tile, B(B−1)/2 for a diagonal tile (the kernel computes i < j there and
 mirrors; K[i, i] comes from the per-image variance chain).  The reference's schedule
 would count B² for a diagonal tile; that figure is reported as
 ``reference_schedule_pairs_per_s`` beside it.
 
-Also on the same JSON line:
+Also on the same JSON line (each in its own slot; a leg that fails records
+{"error": ...} there and the line still prints):
   roofline           the whole-network kernel (net_kernel, fp64 VALU-bound): credited
                      direct-stencil flops vs the fp64 peak, plus the VALU issue
                      utilisation and HBM traffic per launch from the committed PMC
-                     passes (profiles/r3/net_pmc.json, rocprofv3)
+                     passes (profiles/r4/net_pmc.json, rocprofv3)
   mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
-  solve              rocSOLVER dpotrf_64 + dpotrs_64 on the assembled 4096² Kxx
+  cifar10            the same harness on configs[4]'s network (3×32×32, Kxx 4096²)
+  solve              rocSOLVER/rocBLAS blocked Cholesky + dpotrs_64 on the assembled Kxx
   fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
                      + solve + predict, row strips per rank, Kxx received into rank 0's
                      matrix point-to-point, solve overlapped with the Kxz strips, only
@@ -32,20 +41,27 @@ Also on the same JSON line:
                      bit-identical to the reference at C1) on the host threads torch
                      is given, with the committed calibration against the reference
 
-Multi-GPU (one process per GPU, torchrun): the Kxx grows with the world
-(n_blocks² half-tile units >= world × the 1-GPU units, divisible by world) and its tiles
-are split over the ranks by evaluated pairs — no data-path collective; per-rank work is
-~constant ("scaling": "weak").  The full-scale legs shard their fixed problems
-("strong"): Kxx strips to rank 0 point-to-point, α broadcast, scores gathered.
+Multi-GPU (one process per GPU): the Kxx grows with the world (n_blocks² half-tile units
+>= world × the 1-GPU units, divisible by world) and its tiles are split over the ranks by
+evaluated pairs — no data-path collective; per-rank work is ~constant ("scaling":
+"weak").  The full-scale legs shard their fixed problems ("strong"): Kxx strips to rank 0
+point-to-point, α broadcast, scores gathered.  Every collective has a timeout
+(CGP_DIST_TIMEOUT_S, default 300 s) and raises instead of hanging; the legs' outcomes are
+exchanged over a gloo side group after each leg, so a failure on any rank is recorded
+and the remaining multi-rank legs are skipped.
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT, os.path.join(ROOT, "tools")]
@@ -62,19 +78,24 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md): 8 TB/s
 FP64_PEAK_TFLOPS = 78.6        # MI355X spec FP64 (vector = matrix); half the FP32 157.3
 SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
 CLOCK_HZ = 2.4e9               # peak engine clock
-PMC_FILE = os.path.join(ROOT, "profiles", "r3", "net_pmc.json")
-CALIB_FILE = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
+# committed PMC passes, newest first (a config missing from a newer file is looked up in
+# the older one)
+PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r4", "r3")]
+CALIB_FILES = [os.path.join(ROOT, "profiles", r, "cpu_calibration.json") for r in ("r4", "r2")]
+DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "300"))
 PIPELINE_NOTE = (
     "cnn_gp.pipeline.classify_distributed: Kxx row strips (B=4096 tiles) balanced by "
     "evaluated pairs, received point-to-point into the full matrix on rank 0 (RCCL with "
-    "nccl); rank 0 factors it (blocked dpotrf/dtrsm/dsyrk, nb 2048) while the other ranks "
-    "build their Kxz row strips (rank 0's share sized to end with them); alpha broadcast, "
-    "scores = Kxz rows @ alpha per rank, only the scores gathered; solver code objects "
-    "loaded on a side thread during the Kxx build; spot check = HIP vs HIP single pairs "
-    "(oracle parity at this geometry: tests/test_gpu_fullgeom.py)")
+    "nccl; that path first runs on the driver's multi-GPU node: every multi-rank run so "
+    "far used gloo ranks sharing one GPU); rank 0 factors it (blocked dpotrf/dtrsm/dsyrk, "
+    "nb 2048) while the other ranks build their Kxz row strips (rank 0's share sized to "
+    "end with them); alpha broadcast, scores = Kxz rows @ alpha per rank, only the scores "
+    "gathered; solver code objects loaded on a side thread during the Kxx build; spot "
+    "check = HIP vs HIP single pairs in the computed orientation (oracle parity at this "
+    "geometry: tests/test_gpu_fullgeom.py, tests/test_gpu_fullscale_bound.py)")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
@@ -87,6 +108,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-probe", action="store_true")
     p.add_argument("--no-second", action="store_true", help="skip the mnist_as_tf leg")
+    p.add_argument("--no-cifar10", action="store_true", help="skip the cifar10 Kxx leg")
     p.add_argument("--no-f32", action="store_true",
                    help="skip the float32 repeat of the Kxx legs")
     p.add_argument("--no-fullscale", action="store_true")
@@ -97,9 +119,108 @@ def parse():
     p.add_argument("--fullscale-n", type=int, default=60000)
     p.add_argument("--cifar10-n", type=int, default=50000)
     p.add_argument("--fullscale-m", type=int, default=10000)
-    p.add_argument("--cpu-seconds", type=float, default=15.0,
-                   help="target duration of the CPU-baseline sample")
-    return p.parse_args()
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="target duration of each CPU-baseline sample")
+    return p.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------------------
+# launcher: --gpus N starts its own N ranks
+# ------------------------------------------------------------------------------------------
+
+def world_error(gpus: int, world: int, n_devices: int, backend: str):
+    """Why this rank set cannot run (a message), or None."""
+    if gpus < 1:
+        return f"--gpus {gpus}: at least one GPU"
+    if world != gpus:
+        return (f"--gpus {gpus} but WORLD_SIZE is {world}: run `python bench.py --gpus "
+                f"{gpus}` (it starts its own ranks) or torchrun with --nproc-per-node {gpus}")
+    if backend == "nccl" and world > 1 and world > n_devices:
+        return (f"--gpus {gpus} needs {gpus} visible GPUs (one rank per GPU over RCCL); "
+                f"{n_devices} visible")
+    return None
+
+
+def launch_cmd(argv, gpus: int, port: int):
+    """The child command of the launcher: one rank per GPU on this node, rendezvous on
+    127.0.0.1 (the container's hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+            "--nproc-per-node", str(gpus), "--master-addr", "127.0.0.1",
+            "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_or_check(args, argv):
+    """None: this process runs the bench (one rank).  An int: the exit status to leave
+    with — the launched ranks' status, or 2 for a refused rank set.  Makes no GPU call
+    (torch.cuda.device_count() does not initialise the runtime on this image), so the
+    launcher's child is a fresh process, never an exec of one that touched the GPU."""
+    backend = os.environ.get("CGP_BENCH_BACKEND", "nccl")
+    env_world = os.environ.get("WORLD_SIZE")
+    world = args.gpus if env_world is None else int(env_world)
+    err = world_error(args.gpus, world, torch.cuda.device_count(), backend)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr, flush=True)
+        return 2
+    if env_world is not None or args.gpus == 1:
+        return None
+    cmd = launch_cmd(argv, args.gpus, free_port())
+    print(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd)
+
+
+# ------------------------------------------------------------------------------------------
+# legs: one failure costs its own slot, not the line
+# ------------------------------------------------------------------------------------------
+
+class Legs:
+    """Runs each measurement leg and agrees on its outcome across the ranks.
+
+    A leg's exception is caught and recorded as {"error": ...} in its slot; with several
+    ranks every rank's outcome is exchanged over a gloo side group (``group``: host
+    memory, its own timeout, independent of the RCCL communicator's state), and once any
+    rank has failed a leg the remaining multi-rank legs are skipped — a collective could
+    otherwise pair with a different leg's on another rank.  CGP_BENCH_FAIL_LEG=<name>[,…]
+    forces a failure (tests of this mechanism)."""
+
+    def __init__(self, world: int = 1, rank: int = 0, group=None):
+        self.world, self.rank, self.group = world, rank, group
+        self.stopped = None
+
+    def run(self, name, fn, multi_rank=True):
+        if self.stopped and multi_rank and self.world > 1:
+            return {"error": f"skipped: leg {self.stopped!r} failed on a rank"}
+        err, out = None, None
+        try:
+            if name in os.environ.get("CGP_BENCH_FAIL_LEG", "").split(","):
+                raise RuntimeError(f"forced failure of leg {name!r} (CGP_BENCH_FAIL_LEG)")
+            out = fn()
+        except Exception as e:                 # noqa: BLE001 — recorded, never swallowed
+            err = f"{type(e).__name__}: {e}"[:1000]
+            print(f"bench.py: rank {self.rank}: leg {name!r} failed", file=sys.stderr)
+            traceback.print_exc(file=sys.stderr)
+            out = None
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        if self.world > 1 and multi_rank:
+            errs = [None] * self.world
+            try:
+                dist.all_gather_object(errs, err, group=self.group)
+            except Exception as e:             # noqa: BLE001
+                errs = [f"leg status exchange failed: {type(e).__name__}: {e}"]
+            bad = {str(r): m for r, m in enumerate(errs) if m}
+            if bad:
+                self.stopped = name
+                return {"error": bad}
+        elif err:
+            return {"error": err}
+        return out
 
 
 def blocks_for_world(n1: int, tile: int, world: int) -> int:
@@ -157,13 +278,22 @@ def load_json(path):
         return None
 
 
+def committed(files, key):
+    """(entry, file) of ``key`` in the newest committed JSON that has it, else (None, None)"""
+    for f in files:
+        v = (load_json(f) or {}).get(key)
+        if v is not None:
+            return v, os.path.relpath(f, ROOT)
+    return None, None
+
+
 def conv_stencil_roofline(model, x, B, reps=5):
     """Conv2d.propagate alone (kernels.py:92-98; no fused ReLU / moments / Sum) — the
     north star's "Conv2d covariance kernel" — at the config's most frequent conv shape, on
     the B·B pair maps of one tile, timed with HIP events on the launch stream; against the
     8 TB/s HBM roof with algorithmic bytes 8·P·(H·W + Ho·Wo).  A torch copy of the same
     input is timed beside it as the achievable-bandwidth reference.  ``traffic``: the
-    committed PMC pass over the same launch (profiles/r3/net_pmc.json "conv_stencil")."""
+    committed PMC pass over the same launch (profiles/r*/net_pmc.json "conv_stencil")."""
     from collections import Counter
     _, C, h, w = x.shape
     plan = model._plan(h, w)
@@ -173,17 +303,20 @@ def conv_stencil_roofline(model, x, B, reps=5):
     if not convs:
         return None
     (k, off, st, (hi, wi), (ho, wo)), _ = convs.most_common(1)[0]
-    P = B * B
+    # the maps of one B = 1024 tile (13 GB of fp64 input at 28²): larger tiles would ask
+    # for B²-sized copies (98 GiB at B = 4096) and the committed PMC pass is of this size
+    Bs = min(B, 1024)
+    P = Bs * Bs
     g = torch.Generator(device="cpu").manual_seed(0)
-    var = torch.rand((2 * B, hi, wi), generator=g, dtype=x.dtype).add_(0.5).to(x.device)
-    xy = (0.5 * (var[:B, None] * var[None, B:]).sqrt()).reshape(P, hi, wi).contiguous()
+    var = torch.rand((2 * Bs, hi, wi), generator=g, dtype=x.dtype).add_(0.5).to(x.device)
+    xy = (0.5 * (var[:Bs, None] * var[None, Bs:]).sqrt()).reshape(P, hi, wi).contiguous()
     del var
     out = torch.empty((P, ho, wo), dtype=x.dtype, device=x.device)
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
     a = N.ConvArgs()
     a.in_, a.out = N.ptr(xy), N.ptr(out)
-    a.nmaps, a.n1, a.n2 = P, B, B
+    a.nmaps, a.n1, a.n2 = P, Bs, Bs
     a.h, a.w, a.ho, a.wo = hi, wi, ho, wo
     a.taps, a.offset, a.stride, a.dilation = k, off, st, 1
     a.weight, a.bias = 1.0 / (k * k), 0.1
@@ -199,7 +332,7 @@ def conv_stencil_roofline(model, x, B, reps=5):
     torch.cuda.empty_cache()
     kname = f"conv{k}s{st}@{hi}->{ho}"
     traffic, pmc_ms = None, None
-    pmc = (load_json(PMC_FILE) or {}).get("conv_stencil")
+    pmc, _ = committed(PMC_FILES, "conv_stencil")
     if pmc and pmc.get("kernel") == kname and pmc.get("maps") == P:
         traffic, pmc_ms = int(pmc["hbm_bytes_per_launch"]), pmc.get("avg_ms")
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -267,13 +400,13 @@ def net_roofline(model, x, cfg_name, timing):
     avg_s = ms * 1e-3 / len(timing)
     traffic = valu = valu_insts = None
     pmc_note = "no committed PMC pass for this config/dtype"
-    pmc = (load_json(PMC_FILE) or {}).get(cfg_name)
+    pmc, pmc_file = committed(PMC_FILES, cfg_name)
     if pmc and pmc.get("dtype") == str(x.dtype):
         traffic = int(pmc["hbm_bytes_per_pair"] * per_launch)
         quad = pmc["valu_active_quadcycles_per_pair"] * per_launch
         valu = round(4 * quad / (SIMDS * CLOCK_HZ * avg_s), 4)
         valu_insts = round(pmc["valu_insts_per_pair"], 1)
-        pmc_note = (f"PMC: {pmc['source']}; per pair: {pmc['hbm_bytes_per_pair']:.0f} HBM "
+        pmc_note = (f"PMC ({pmc_file}): {pmc['source']}; per pair: {pmc['hbm_bytes_per_pair']:.0f} HBM "
                     f"bytes, {pmc['valu_insts_per_pair']:.0f} VALU wave-instructions")
     kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
     return {"bound": "valu_f64", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
@@ -374,7 +507,12 @@ def cpu_baseline(cfg_name, dtype, seconds):
                sample=f"one {side}x{side} Kxz tile of {cfg_name} ({side * side} pairs, {dtn}) "
                       f"through oracle/torch_cpu.py (the reference's torch op sequence) "
                       f"in {el:.1f} s on {torch.get_num_threads()} threads")
-    cal = load_json(CALIB_FILE)
+    cal, cal_file = None, None
+    for f in CALIB_FILES:
+        c = load_json(f)
+        if c and any(k["config"] == cfg_name for k in c["cases"]):
+            cal, cal_file = c, os.path.relpath(f, ROOT)
+            break
     if cal:
         case = next((c for c in cal["cases"] if c["config"] == cfg_name and c["dtype"] == dtn),
                     None)
@@ -384,7 +522,7 @@ def cpu_baseline(cfg_name, dtype, seconds):
                 "reference_pairs_per_s_build_container": case["reference_pairs_per_s"],
                 "threads": cal["threads"], "cpu_model": cal["cpu_model"],
                 "max_rel_diff_vs_reference": case["max_rel_diff"],
-                "source": "profiles/r2/cpu_calibration.json (tools/calibrate_cpu.py)"}
+                "source": f"{cal_file} (tools/calibrate_cpu.py)"}
             res["reference_equivalent_pairs_per_s"] = round(
                 res["value"] / case["restatement_over_reference"], 1)
     return res
@@ -403,6 +541,7 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     all_tiles = tile_schedule(n_total, None, B, 0, 1)
     tiles = balanced_split(all_tiles, B, n_total, world)[rank]
     evaluated = sum(tile_eval_pairs(t, B, n_total) for t in all_tiles)
+    mine = sum(tile_eval_pairs(t, B, n_total) for t in tiles)
     ref_sched = sum(min(B, n_total - i * B) * min(B, n_total - j * B) for _, i, j in all_tiles)
     K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
 
@@ -433,6 +572,7 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    mine_s = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
@@ -445,11 +585,50 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
                 elapsed=elapsed, value=evaluated * steps / elapsed,
                 ref_sched_value=ref_sched * steps / elapsed, evaluated=evaluated,
                 ms_step=elapsed / steps * 1e3,
-                unique=n_total * (n_total + 1) / 2 * steps / elapsed, timing=timing)
+                unique=n_total * (n_total + 1) / 2 * steps / elapsed, timing=timing,
+                rank_stats={"rank": rank, "tiles": len(tiles), "pairs_per_step": mine,
+                            "ms_per_step": round(mine_s / steps * 1e3, 3)})
 
 
-def main():
-    args = parse()
+def gather_rank_stats(stats, world, group):
+    """every rank's stats dict, on every rank (gloo side group), rank order"""
+    if world <= 1:
+        return [stats]
+    out = [None] * world
+    dist.all_gather_object(out, stats, group=group)
+    return out
+
+
+def kxx_leg(cfg_name, args, B, world, rank, dev, dtype, backend, probe, group, steps,
+            with_cpu):
+    """configs[2] / configs[4]'s network on the headline's harness (Kxx 4096², B = 1024),
+    with its own roofline object and CPU baseline"""
+    r2 = time_config(cfg_name, args.n, B, steps, 1, world, rank, dev, dtype, backend, probe)
+    del r2["K"]
+    ranks = gather_rank_stats(r2["rank_stats"], world, group)
+    if rank != 0:
+        return None
+    out = {
+        "value": round(r2["value"], 1), "unit": "pairs/s",
+        "ms_per_step": round(r2["ms_step"], 3), "steps": steps,
+        "unique_entries_per_s": round(r2["unique"], 1),
+        "reference_schedule_pairs_per_s": round(r2["ref_sched_value"], 1),
+        "config": {"workload": f"{cfg_name} Kxx {r2['n_total']}x{r2['n_total']}, "
+                               f"tiles {B}", "pairs_per_step": r2["evaluated"]},
+        "ranks": ranks,
+        "roofline": net_roofline(r2["model"], r2["X"][:B], cfg_name, r2["timing"])
+        if probe else None}
+    if with_cpu:
+        out["cpu_baseline"] = cpu_baseline(cfg_name, dtype, args.cpu_seconds)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = launch_or_check(args, argv)
+    if rc is not None:
+        return rc
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -460,171 +639,198 @@ def main():
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    status = None
     if world > 1:
+        # a collective that does not complete raises after the timeout instead of hanging
+        # until the driver kills the run (blocking wait: the RCCL watchdog would abort)
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        tmo = datetime.timedelta(seconds=DIST_TIMEOUT_S)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+        status = dist.new_group(backend="gloo",
+                                timeout=datetime.timedelta(seconds=2 * DIST_TIMEOUT_S + 60))
+    legs = Legs(world, rank, status)
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
     B = args.tile
     probe = not args.no_probe
-
-    r = time_config(args.config, args.n, B, args.steps, args.warmup, world, rank, dev, dtype,
-                    backend, probe)
-    n_total = r["n_total"]
     extra = {}
 
+    def put(name, value):
+        if rank == 0 and value is not None:
+            extra[name] = value
+
+    # --- the headline: BASELINE configs[1] ---
+    r = legs.run("headline", lambda: time_config(args.config, args.n, B, args.steps,
+                                                 args.warmup, world, rank, dev, dtype,
+                                                 backend, probe))
+    failed = "error" in r
+    ranks = None
+    if not failed:
+        ranks = legs.run("rank_stats", lambda: gather_rank_stats(r["rank_stats"], world,
+                                                                   status))
+    n_total = None if failed else r["n_total"]
+
     # --- solve of the assembled Kxx (single GPU) ---
-    if rank == 0 and world == 1 and not args.no_solve:
+    def solve_leg():
         g = torch.Generator().manual_seed(1)
         labels = torch.randint(0, 10, (n_total,), generator=g)
         Y = cnn_gp.one_hot_pm1(labels, 10).to(dev)
         # untimed warm-up solve at the full size (rocBLAS/rocSOLVER load the code objects
         # of each blocked path on first use)
         cnn_gp.solve_system(r["K"], Y, jitter=1e-6)
-        times = []
+        times, phases = [], []
         for _ in range(3):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             cnn_gp.solve_system(r["K"], Y, jitter=1e-6)      # Kxx kept: copy + factor
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t1)
-        t_solve = min(times)
-        extra["solve"] = {"n": n_total, "s": round(t_solve, 4),
-                          "tflops": round(n_total ** 3 / 3 / t_solve / 1e12, 3),
-                          "peak_tflops": FP64_PEAK_TFLOPS,
-                          "note": "dpotrf_64 + dpotrs_64 (10 rhs) on a device copy of Kxx "
-                                  "(NaN lower triangle), best of 3 after a warm-up"}
-        extra["build_solve_wall_s"] = round(r["ms_step"] / 1e3 + t_solve, 4)
+            phases.append(cnn_gp.solve_phases(dev))
+        k = min(range(3), key=lambda q: times[q])
+        t_solve = times[k]
+        ph = {p: round(v, 5) for p, v in phases[k].items()}
+        return {"n": n_total, "s": round(t_solve, 4),
+                "tflops": round(n_total ** 3 / 3 / t_solve / 1e12, 3),
+                "factor_tflops": round(n_total ** 3 / 3 / max(ph["factor_s"], 1e-9) / 1e12, 3),
+                "peak_tflops": FP64_PEAK_TFLOPS, **ph,
+                "copy_and_transposes_s": round(t_solve - sum(ph.values()), 5),
+                "build_solve_wall_s": round(r["ms_step"] / 1e3 + t_solve, 4),
+                "note": "blocked dpotrf/dtrsm/dsyrk + dpotrs_64 (10 rhs) on a device copy "
+                        "of Kxx (NaN lower triangle), best of 3 after a warm-up; phases "
+                        "from HIP events inside cgp_chol_solve_f64"}
+
+    if not failed and rank == 0 and world == 1 and not args.no_solve:
+        put("solve", legs.run("solve", solve_leg, multi_rank=False))
 
     # --- dominant kernel, timed live ---
     roof = None
-    if rank == 0 and probe:
-        roof = net_roofline(r["model"], r["X"][:B], args.config, r["timing"])
-        with torch.no_grad():
-            stencil = conv_stencil_roofline(r["model"], r["X"][:B], B)
-        if stencil is not None:
-            extra["conv_stencil_roofline"] = stencil
-    del r["K"]
+    if not failed and rank == 0 and probe:
+        roof = legs.run("roofline", lambda: net_roofline(r["model"], r["X"][:B], args.config,
+                                                         r["timing"]), multi_rank=False)
+
+        def stencil():
+            with torch.no_grad():
+                return conv_stencil_roofline(r["model"], r["X"][:B], B)
+        put("conv_stencil_roofline", legs.run("conv_stencil_roofline", stencil,
+                                              multi_rank=False))
+    if not failed:
+        del r["K"]
     torch.cuda.empty_cache()
 
-    # --- BASELINE configs[2]: the ResNet-GP on the same harness ---
+    # --- BASELINE configs[2] (ResNet-GP) and configs[4]'s network on the same harness ---
+    cpu_ok = world == 1 and not args.no_cpu
     if not args.no_second and args.config != "mnist_as_tf":
-        r2 = time_config("mnist_as_tf", args.n, B, max(2, args.steps // 4), 1, world, rank,
-                         dev, dtype, backend, probe)
-        del r2["K"]
-        if rank == 0:
-            extra["mnist_as_tf"] = {
-                "value": round(r2["value"], 1), "unit": "pairs/s",
-                "ms_per_step": round(r2["ms_step"], 3),
-                "unique_entries_per_s": round(r2["unique"], 1),
-                "reference_schedule_pairs_per_s": round(r2["ref_sched_value"], 1),
-                "config": {"workload": f"mnist_as_tf Kxx {r2['n_total']}x{r2['n_total']}, "
-                                       f"tiles {B}", "pairs_per_step": r2["evaluated"]},
-                "roofline": net_roofline(r2["model"], r2["X"][:B], "mnist_as_tf",
-                                         r2["timing"]) if probe else None}
-            if world == 1 and not args.no_cpu:
-                extra["mnist_as_tf"]["cpu_baseline"] = cpu_baseline(
-                    "mnist_as_tf", dtype, args.cpu_seconds)
-        torch.cuda.empty_cache()
+        put("mnist_as_tf", legs.run("mnist_as_tf", lambda: kxx_leg(
+            "mnist_as_tf", args, B, world, rank, dev, dtype, backend, probe, status,
+            max(2, args.steps // 4), cpu_ok)))
+    if not args.no_cifar10 and args.config != "cifar10":
+        put("cifar10", legs.run("cifar10", lambda: kxx_leg(
+            "cifar10", args, B, world, rank, dev, dtype, backend, probe, status,
+            max(2, args.steps // 4), cpu_ok)))
 
-    # --- the same two workloads at the reference pipeline's own kernel precision ---
+    # --- the same workloads at the reference pipeline's own kernel precision ---
     # (exp_mnist_resnet/save_kernel.py runs the float32 model; kernel_save_tools.py:21
     # stores K as float32).  Reported beside the fp64 headline, never as `value`.
     if not args.no_f32 and dtype == torch.float64:
-        f32 = {}
-        for name in ((args.config,) if args.no_second or args.config == "mnist_as_tf"
-                     else (args.config, "mnist_as_tf")):
-            r3 = time_config(name, args.n, B, max(2, args.steps // 2), 1, world, rank, dev,
-                             torch.float32, backend, False)
-            del r3["K"]
-            f32[name] = {"value": round(r3["value"], 1), "unit": "pairs/s",
-                         "ms_per_step": round(r3["ms_step"], 3),
-                         "pairs_per_step": r3["evaluated"]}
-            torch.cuda.empty_cache()
-        if rank == 0:
+        def f32_leg():
+            f32 = {}
+            for name in ((args.config,) if args.no_second or args.config == "mnist_as_tf"
+                         else (args.config, "mnist_as_tf")):
+                r3 = time_config(name, args.n, B, max(2, args.steps // 2), 1, world, rank, dev,
+                                 torch.float32, backend, False)
+                del r3["K"]
+                f32[name] = {"value": round(r3["value"], 1), "unit": "pairs/s",
+                             "ms_per_step": round(r3["ms_step"], 3),
+                             "pairs_per_step": r3["evaluated"]}
+                torch.cuda.empty_cache()
             f32["note"] = ("float32 model and images, as the reference's save_kernel.py runs "
                            "them; same Kxx harness as the fp64 legs.  Entries stay within "
                            "3e-7 relative of the fp64 kernel (tests/test_gpu_parity.py "
                            "test_f32_kernel_within_north_star_tolerance; north star 1e-5)")
-            extra["f32"] = f32
+            return f32 if rank == 0 else None
+        put("f32", legs.run("f32", f32_leg))
 
-    # --- BASELINE configs[3]: the full-scale ResNet-GP pipeline ---
-    if not args.no_fullscale and dtype == torch.float64:
+    # --- BASELINE configs[3] / [4]: the full-scale ResNet-GP pipelines ---
+    def fullscale_leg(config, n, kernel_dtype, data, note):
         from fullscale import fullscale
         t0 = time.perf_counter()
-        fs = fullscale("mnist_as_tf", args.fullscale_n, args.fullscale_m, 4096, rank=rank,
-                       world=world, dev=dev)
-        if rank == 0:
-            fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
-            fs["data"] = "synthetic MNIST-like (k/255, 60% zeros, 4-px zero border)"
-            fs["note"] = PIPELINE_NOTE
-            extra["fullscale"] = fs
-        torch.cuda.empty_cache()
+        fs = fullscale(config, n, args.fullscale_m, 4096, rank=rank, world=world, dev=dev,
+                       kernel_dtype=kernel_dtype, stats_group=status)
+        if rank != 0:
+            return None
+        fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
+        fs["data"] = data
+        fs["note"] = note
+        return fs
+
+    mnist_data = "synthetic MNIST-like (k/255, 60% zeros, 4-px zero border)"
+    if not args.no_fullscale and dtype == torch.float64:
+        put("fullscale", legs.run("fullscale", lambda: fullscale_leg(
+            "mnist_as_tf", args.fullscale_n, torch.float64, mnist_data, PIPELINE_NOTE)))
         if not args.no_fullscale_f32:
             # the same pipeline at the reference pipeline's own kernel precision
             # (save_kernel.py runs the float32 model; K stored float32, widened to float64
             # for the solve by classify_gp.py's load_kern)
-            t0 = time.perf_counter()
-            fs = fullscale("mnist_as_tf", args.fullscale_n, args.fullscale_m, 4096,
-                           rank=rank, world=world, dev=dev, kernel_dtype=torch.float32)
-            if rank == 0:
-                fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
-                fs["note"] = ("kernels in float32 as exp_mnist_resnet/save_kernel.py runs "
-                              "them; K widened to float64 on the device for the rocSOLVER "
-                              "solve; spot_vs_f64_max_rel_err = float32 entries against "
-                              "the float64 model (north-star tolerance 1e-5)")
-                extra["fullscale_f32"] = fs
-            torch.cuda.empty_cache()
-
-    # --- BASELINE configs[4]: cifar10 ResNet-GP, Kxx 50 000² on 3×32×32 ---
+            put("fullscale_f32", legs.run("fullscale_f32", lambda: fullscale_leg(
+                "mnist_as_tf", args.fullscale_n, torch.float32, mnist_data,
+                "kernels in float32 as exp_mnist_resnet/save_kernel.py runs them; K widened "
+                "to float64 on the device for the rocSOLVER solve; spot_vs_f64_max_rel_err "
+                "= float32 entries against the float64 model (north-star tolerance 1e-5)")))
     if not args.no_fullscale_cifar10 and dtype == torch.float64:
-        from fullscale import fullscale
-        t0 = time.perf_counter()
-        fs = fullscale("cifar10", args.cifar10_n, args.fullscale_m, 4096, rank=rank,
-                       world=world, dev=dev)
-        if rank == 0:
-            fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
-            fs["data"] = "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)"
-            fs["note"] = ("BASELINE configs[4] (configs/cifar10.py:4-47 architecture). " +
-                          PIPELINE_NOTE)
-            extra["fullscale_cifar10"] = fs
-        torch.cuda.empty_cache()
+        put("fullscale_cifar10", legs.run("fullscale_cifar10", lambda: fullscale_leg(
+            "cifar10", args.cifar10_n, torch.float64,
+            "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)",
+            "BASELINE configs[4] (configs/cifar10.py:4-47 architecture). " + PIPELINE_NOTE)))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.config, dtype, args.cpu_seconds)
+    if rank == 0 and cpu_ok:
+        cpu = legs.run("cpu_baseline", lambda: cpu_baseline(args.config, dtype,
+                                                            args.cpu_seconds),
+                       multi_rank=False)
 
     if rank == 0:
         line = {
             "metric": "kernel entries/s (N×M pairs) + full-Kxx build+solve wall-clock, "
                       "MNIST 28×28",
-            "value": round(r["value"], 1),
+            "value": None if failed else round(r["value"], 1),
             "unit": "pairs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(r["ms_step"], 3),
+            "ms_per_step": None if failed else round(r["ms_step"], 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (torch.rand seed 0, 28x28x1)",
             "config": {"workload": f"{args.config} Kxx {n_total}x{n_total}, tiles {B}",
-                       "n": n_total, "tile": B, "tiles_total": len(r["all_tiles"]),
-                       "tiles_rank0": len(r["tiles"]), "pairs_per_step": r["evaluated"],
+                       "n": n_total, "tile": B,
+                       "tiles_total": None if failed else len(r["all_tiles"]),
+                       "tiles_rank0": None if failed else len(r["tiles"]),
+                       "pairs_per_step": None if failed else r["evaluated"],
                        "parallelism": f"tiles-dp{world}"},
+            "world": world,
+            "backend": backend if world > 1 else None,
             "value_counts": "pairs the device evaluates: i < j on diagonal tiles",
-            "reference_schedule_pairs_per_s": round(r["ref_sched_value"], 1),
-            "unique_entries_per_s": round(r["unique"], 1),
+            "reference_schedule_pairs_per_s": None if failed else round(r["ref_sched_value"], 1),
+            "unique_entries_per_s": None if failed else round(r["unique"], 1),
+            "ranks": ranks,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if failed:
+            line["error"] = r["error"]
         line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        try:
+            dist.destroy_process_group()
+        except Exception:                      # noqa: BLE001 — after a failed leg
+            pass
+    return 1 if failed else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -133,6 +133,7 @@ SIGNATURES = {
     "cgp_transpose_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_chol_solve_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,
                                   ctypes.POINTER(_i64), _vp]),
+    "cgp_chol_last_phases": (_i32, [_vp, ctypes.POINTER(_f64)]),
     "cgp_gemm_f64": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_pred_var_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp]),

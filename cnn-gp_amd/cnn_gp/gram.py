@@ -48,6 +48,18 @@ def _rows(X, lo, hi):
     return torch.stack([X[k][0] for k in range(lo, hi)])
 
 
+def row_slice(X, lo, hi):
+    """Images lo:hi of X as an image set of the same kind (tensor, TensorDataset-like or
+    Dataset), for building a strip from only the rows it reads."""
+    if isinstance(X, torch.Tensor):
+        return X[lo:hi]
+    if hasattr(X, "tensors"):
+        from torch.utils.data import TensorDataset
+        return TensorDataset(*(t[lo:hi] for t in X.tensors))
+    from torch.utils.data import Subset
+    return Subset(X, range(lo, hi))
+
+
 def _default_device(device):
     if device is not None:
         return torch.device(device)
@@ -137,6 +149,8 @@ def _fill_tiles(kern, X, src2, X2, tiles, view):
     """Evaluate ``tiles`` into view(t) (a [rows, cols] slice of the output each): from one
     bound build when kern is a ModelKern with a whole-network program, else one kern call
     per tile copied into place."""
+    if not tiles:                 # an empty strip: nothing to bind
+        return
     bound = kern.bind(X, X2) if isinstance(kern, ModelKern) else None
     for t in tiles:
         if bound is not None:

@@ -200,7 +200,7 @@ class NetPlan:
             outs = sorted(v for v, pi in prod.items() if pi < hi <= last.get(v, -1)) \
                 if hi < len(lowered) else []
             st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
-            # the two-pair workgroup holds cgp_net_units(2) one-pair arenas (CGP_NET_SPLIT)
+            # the two-pair workgroup holds cgp_net_units(2) one-pair arenas
             if np_ == 2 and st.lds_elems * itemsize * lib.cgp_net_units(2) > MAX_LDS_BYTES:
                 st = self._lower(lowered, lo, hi, 1, ins, outs, last, dual, itemsize)
             self.stages.append(st)

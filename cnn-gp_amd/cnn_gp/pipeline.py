@@ -29,7 +29,7 @@ from typing import Callable, Optional
 import torch
 import torch.distributed as dist
 
-from .gram import gather_strips, gram_strip, strip_cost, strip_plan
+from .gram import gather_strips, gram_strip, row_slice, strip_cost, strip_plan
 
 __all__ = ("classify_distributed", "kxz_weights", "widening_matrix", "widen_in_place")
 
@@ -58,6 +58,8 @@ def widen_in_place(buf: torch.Tensor, narrow: torch.Tensor,
     one non-overlapping block (default dst.copy_(src); the device path passes
     solve.cast_into, the HIP cgp_cast_f32_f64).  Returns buf."""
     cast = cast or (lambda s, d: d.copy_(s))
+    if tail_rows < 1:
+        raise ValueError(f"tail_rows {tail_rows}: at least one row (the halving must end)")
     n = buf.shape[0]
     i0 = 0
     while i0 < n:
@@ -70,8 +72,11 @@ def widen_in_place(buf: torch.Tensor, narrow: torch.Tensor,
     return buf
 
 
+SOLVE_TFLOPS = 45.0     # the blocked Cholesky at n = 50-60 k in the full-scale runs (47-49)
+
+
 def kxz_weights(world: int, n: int, m: int, kernel_pairs_per_s: float,
-                solve_tflops: float = 30.0, dst: int = 0):
+                solve_tflops: float = SOLVE_TFLOPS, dst: int = 0):
     """Kxz row shares: rank ``dst`` also solves, so its share s0 satisfies
     solve + s0·T = (1 − s0)/(world − 1)·T, T = m·n / rate (the whole Kxz on one GPU),
     clipped to [0, 1/world].  None (equal shares) at world size 1."""
@@ -112,9 +117,11 @@ def _sync(dev):
 def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          scores: Callable, batch_size: int = 4096, group=None, dst: int = 0,
                          device=None, dtype=torch.float64, out_dtype=torch.float64,
-                         gather_kxz: bool = False, kxz_share=None, solve_tflops: float = 30.0,
+                         gather_kxz: bool = False, kxz_share=None,
+                         solve_tflops: float = SOLVE_TFLOPS,
                          widen: Optional[Callable] = None, log: Optional[Callable] = None,
-                         warm: Optional[Callable] = None, cast: Optional[Callable] = None):
+                         warm: Optional[Callable] = None, cast: Optional[Callable] = None,
+                         rank_times: Optional[dict] = None):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
 
@@ -131,7 +138,13 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     matrix solve saw), Kxz (when gather_kxz), dst's own Kxz rows (``kxz_rows``,
     ``Kxz_rows``), timings, the plans and the device memory peaks (overall, and from the
     end of the Kxx build: the gather, the solve and the Kxz phase); None on the other
-    ranks."""
+    ranks.  ``rank_times`` (optional dict) is filled on EVERY rank with that rank's own
+    phase times and pairs (kxx_s, gather_kxx_s, kxz_s, predict_s, kxx_pairs, kxz_pairs).
+
+    Each rank binds only the images its strips read: a Kxx strip [r0, r1) touches rows
+    and columns >= r0 (X[r0:]), a Kxz strip [z0, z1) the images Z[z0:z1] against all of
+    X — the tiles and their order are those of the full sets (gram.strip_tiles anchors
+    them at r0)."""
     conv = widen or (lambda t: t.to(out_dtype))
     dev = torch.device(device) if device is not None else (
         torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
@@ -162,15 +175,21 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
             K.fill_(float("nan"))
         else:
             K = torch.full((n, n), float("nan"), dtype=dtype, device=dev)
-        _, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), out=K[r0:r1], dtype=dtype)
+        rows_out = K[r0:r1]
     else:
-        strip, _, px = gram_strip(kern, X, None, batch_size, (r0, r1), device=dev,
-                                  dtype=dtype)
+        strip = torch.full((r1 - r0, n), float("nan"), dtype=dtype, device=dev)
+        rows_out = strip
+    # the strip's upper part [r0, r1) x [r0, n) from the images X[r0:] (strip_tiles in
+    # local coordinates: the same tiles as over all of X, shifted by r0)
+    _, _, px = gram_strip(kern, row_slice(X, r0, n), None, batch_size, (0, r1 - r0),
+                          out=rows_out[:, r0:], dtype=dtype)
     _sync(dev)
     t_kxx = time.perf_counter() - t0
     if warming is not None:           # done long before on a full-size build; its 1.2 GB
         warming.join()                # identity must not count in the next phase's peak
         warming = None
+        if dev.type == "cuda":        # nor stay reserved on the warm-up thread's stream
+            torch.cuda.empty_cache()
     if dev.type == "cuda":
         res["peak_bytes_kxx_build"] = int(torch.cuda.max_memory_allocated(dev))
         torch.cuda.reset_peak_memory_stats(dev)      # next: the gather and the solve
@@ -206,6 +225,8 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
         else:
             Kd = conv(K)
         del K, Kwide
+        _sync(dev)
+        res["widen_s"] = round(time.perf_counter() - t2, 3)
         try:
             alpha = solve(Kd, Y.to(dev, out_dtype))
         except Exception as e:      # e.g. LinAlgError (not PD): the other ranks must not
@@ -223,10 +244,11 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     Kz_full = None
     if gather_kxz and rank == dst:
         Kz_full = torch.full((m, n), float("nan"), dtype=dtype, device=dev)
-        Kz, _, pz = gram_strip(kern, Z, X, batch_size, (z0, z1), out=Kz_full[z0:z1],
-                               dtype=dtype)
+        Kz, _, pz = gram_strip(kern, row_slice(Z, z0, z1), X, batch_size, (0, z1 - z0),
+                               out=Kz_full[z0:z1], dtype=dtype)
     else:
-        Kz, _, pz = gram_strip(kern, Z, X, batch_size, (z0, z1), device=dev, dtype=dtype)
+        Kz, _, pz = gram_strip(kern, row_slice(Z, z0, z1), X, batch_size, (0, z1 - z0),
+                               device=dev, dtype=dtype)
     _sync(dev)
     res["kxz_s_rank"] = round(time.perf_counter() - t3, 3)
     res["kxz_pairs_rank"] = pz
@@ -269,6 +291,11 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
         done = _max_over_ranks(done, dev, group)
     res["kxx_to_kxz_s"] = round(done, 3)
     res["total_s"] = round(time.perf_counter() - t0, 3)
+    if rank_times is not None:
+        rank_times.update(rank=rank, kxx_s=res["kxx_s_rank"], kxx_pairs=px,
+                          gather_kxx_s=res["gather_kxx_s"], kxz_s=res["kxz_s_rank"],
+                          kxz_pairs=pz, kxz_rows=[z0, z1], kxx_rows=[r0, r1],
+                          predict_s=res["predict_s"])
     if rank != dst:
         return None
     res.update(alpha=alpha, scores=full_sc, pred=full_sc.argmax(1), Kxz=Kz_full,

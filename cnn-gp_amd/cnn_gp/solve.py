@@ -16,7 +16,7 @@ from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
            "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores",
-           "cast_into")
+           "cast_into", "solve_phases")
 
 
 def _device():
@@ -72,6 +72,16 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
         N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
     sol = sol.reshape(n) if vec else sol
     return sol.to(Y.device)
+
+
+def solve_phases(device=None) -> dict:
+    """Seconds spent in the phases of the last solve_system on ``device`` (HIP events on
+    its stream, cgp_chol_last_phases): jitter (diag_add), factor (the Cholesky), potrs."""
+    dev = torch.device(device) if device is not None else _device()
+    ms = (N._f64 * 3)()
+    with torch.cuda.device(dev):
+        N.check(N.load().cgp_chol_last_phases(_stream(dev), ms), "cgp_chol_last_phases")
+    return {"jitter_s": ms[0] * 1e-3, "factor_s": ms[1] * 1e-3, "potrs_s": ms[2] * 1e-3}
 
 
 def warm_up_solver(device=None, background: bool = True):

@@ -179,18 +179,14 @@ constexpr PolyCoef poly_coef(bool quartered) {
 static __constant__ PolyCoef kReluPolyTabD = poly_coef(false);
 static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 
-// Range-adaptive ReLU (CGP_RELU_ADAPT, default on): lower-degree fits of P on x in
-// [0, kReluAdaptX0/1/2] = [0, 1/8], [0, 1/4], [0, 3/8] (degrees 7, 9, 11) at the error bound
-// of the full degree-13 fit (5.8e-15 / 8.2e-15 / 8.6e-15 vs 1.6e-14; tools/fit_relu_poly.py
-// ADAPT), quartered like kReluPolyTabDq.  relu_q_n takes the shortest one whose interval
-// holds every active lane's pixels of the wave (a wave-uniform branch).  Deep layers have
-// |rho| near 1 (x small): on MNIST-like pairs the ConvNet's ReLUs 2-7 have x <= 0.24 and its
-// last four x <= 0.125.  One-pair code votes over the wave (AD 1 in relu_n):
-// there a wave holds one pair's pixels, so a pair's result never depends on the other
-// pairs of its tile; multi-pair stages vote per pair segment (AD 2, CGP_RELU_ADAPT_MP).
-#ifndef CGP_RELU_ADAPT
-#define CGP_RELU_ADAPT 1
-#endif
+// Range-adaptive ReLU: lower-degree fits of P on x in [0, kReluAdaptX0/1/2] = [0, 1/8],
+// [0, 1/4], [0, 3/8] (degrees 7, 9, 11) at the error bound of the full degree-13 fit
+// (5.8e-15 / 8.2e-15 / 8.6e-15 vs 1.6e-14; tools/fit_relu_poly.py ADAPT), quartered like
+// kReluPolyTabDq.  relu_q_n takes the shortest one whose interval holds every pixel of its
+// vote group (a uniform branch).  Deep layers have |rho| near 1 (x small): on MNIST-like
+// pairs the ConvNet's ReLUs 2-7 have x <= 0.24 and its last four x <= 0.125.
+// Measured and not kept: every degree 6-13 by a binary search of votes, one
+// unrolled degree-13 chain entered at the wave's degree, Horner chains as asm blocks.
 template <int D>
 struct AdaptCoef {
     double c[D + 1];
@@ -209,74 +205,20 @@ static __constant__ AdaptCoef<kReluAdaptDeg0> kReluAdaptTab0 = adapt_coef<kReluA
 static __constant__ AdaptCoef<kReluAdaptDeg1> kReluAdaptTab1 = adapt_coef<kReluAdaptDeg1>(kReluAdaptP1);
 static __constant__ AdaptCoef<kReluAdaptDeg2> kReluAdaptTab2 = adapt_coef<kReluAdaptDeg2>(kReluAdaptP2);
 
-// Per-degree polynomials (relu_poly.h kReluChainP: degrees 6-13, each fitted on [0, X_d] at
-// or below the degree-13 bound), all in one row layout: row r = degree d = kReluChainD0 + r
-// holds the top coefficient a_d at [0] and a_(13-j) at [j] for the steps j >= 14 - d it runs,
-// so every degree's Horner steps read the same SGPR positions.  Two ways to run them:
-//  * CGP_RELU_FINE (A/B, off): the wave's degree from a binary search of votes (three per
-//    ReLU site), then that degree's own unrolled chain (one per degree in the code);
-//    −1% VALU instructions, time within ±1% (cifar10 −2%; profiles/r3/ab_r3p_relu_fine.log);
-//  * CGP_RELU_CHAIN (A/B, off): ONE unrolled degree-13 chain entered at step 14 - d; the
-//    code holds one chain per ReLU site (measured: code size is not a cost, and the chain's
-//    coefficient SGPRs add spills).
-#ifndef CGP_RELU_FINE
-#define CGP_RELU_FINE 0
-#endif
-#ifndef CGP_RELU_CHAIN
-#define CGP_RELU_CHAIN 0
-#endif
-constexpr int kChainD0 = kReluChainD0;
-constexpr int kChainRows = 14 - kChainD0;
-static_assert(sizeof(kReluChainP) == kChainRows * 14 * sizeof(double), "chain table shape");
-static_assert(sizeof(kReluChainX) == (kChainRows - 1) * sizeof(double), "chain thresholds");
-struct ChainCoef {
-    double c[kChainRows][14];
-};
-constexpr ChainCoef chain_coef() {
-    ChainCoef t{};
-    for (int r = 0; r < kChainRows; ++r)
-        for (int j = 0; j < 14; ++j) {
-            const int k = j == 0 ? kChainD0 + r : 13 - j;   // the power this entry multiplies
-            double v = kReluChainP[r][j] * 0.0625;
-            for (int n = 0; n < k; ++n) v *= 0.25;
-            t.c[r][j] = v;
-        }
-    return t;
-}
-static __constant__ ChainCoef kReluChainTab = chain_coef();
-
 typedef const __attribute__((address_space(4))) double* ConstD;   // scalar-loadable
 struct PolyTab {
     ConstD d, dq;
-#if CGP_RELU_ADAPT
     ConstD a0, a1, a2;
-#endif
-#if CGP_RELU_CHAIN || CGP_RELU_FINE
-    ConstD ch;
-#endif
 };
 __device__ __forceinline__ PolyTab poly_table() {
     ConstD p = (ConstD)kReluPolyTabD.c;
     ConstD q = (ConstD)kReluPolyTabDq.c;
     asm volatile("" : "+s"(p), "+s"(q));
-#if CGP_RELU_ADAPT && (CGP_RELU_CHAIN || CGP_RELU_FINE)
-    ConstD a0 = (ConstD)kReluAdaptTab0.c;
-    ConstD a1 = (ConstD)kReluAdaptTab1.c;
-    ConstD a2 = (ConstD)kReluAdaptTab2.c;
-    ConstD ch = (ConstD)&kReluChainTab.c[0][0];
-    // every table pointer opaque: a known address lets the compiler hoist the coefficient
-    // loads out of the pair loop and keep them all in SGPRs (spills)
-    asm volatile("" : "+s"(a0), "+s"(a1), "+s"(a2), "+s"(ch));
-    return PolyTab{p, q, a0, a1, a2, ch};
-#elif CGP_RELU_ADAPT
     ConstD a0 = (ConstD)kReluAdaptTab0.c;
     ConstD a1 = (ConstD)kReluAdaptTab1.c;
     ConstD a2 = (ConstD)kReluAdaptTab2.c;
     asm volatile("" : "+s"(a0), "+s"(a1), "+s"(a2));
     return PolyTab{p, q, a0, a1, a2};
-#else
-    return PolyTab{p, q};
-#endif
 }
 // r·u + c with c in an SGPR pair: the VOP3 form (the compiler would copy c to VGPRs
 // for v_fmac_f64 instead)
@@ -357,24 +299,9 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 // sqrt(t) = T·r·(3 − T·r·r), and |cq|·Y = |c|/sqrt(t) = |rho|.  With x4 = 4x = 2 − 2|rho|,
 // 4·sqrt(x) = x4·h·(3 − x4·h·h), h = rsq(x4), the polynomial term is
 // sqrt(t)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/16 at x4/4, and max(c, 0)/2 = cq + |cq|.
-// CGP_HORNER_ASM (A/B option): the whole chain as one inline-asm block (horner_asm.h,
-// tools/gen_horner_asm.py) — one asm per FMA makes the compiler pad every step boundary
-// with an s_nop, since it cannot see inside the blocks
-#ifndef CGP_HORNER_ASM
-#define CGP_HORNER_ASM 0
-#endif
-#if CGP_HORNER_ASM
-#include "horner_asm.h"
-#endif
 // R interleaved Horner chains of degree D with SGPR coefficients t[0..D]
 template <int R, int D>
 __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], ConstD t) {
-#if CGP_HORNER_ASM
-    if constexpr ((R == 7 || R == 4 || R == 3) && (D == 7 || D == 9 || D == 11 || D == 13)) {
-        horner_asm<R, D>(p, u, t);
-        return;
-    }
-#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) p[r] = fma_sc(t[D], u[r], t[D - 1]);
 #pragma unroll
@@ -384,71 +311,12 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
         for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
     }
 }
-#if CGP_RELU_CHAIN || CGP_RELU_FINE
-// one-chain form: degree d (wave-uniform) of table row t: the first step
-// p = a_d·x4 + a_(d-1) reads its addend at t[14 - d] (a scalar load at a uniform offset), so
-// every degree starts at the same instruction and no per-pixel copy of a_d is needed; steps
-// 15 - d .. 13 follow, those below 15 - kChainD0 under uniform branches on d
-template <int R>
-__device__ __forceinline__ void horner_chain(double (&p)[R], const double (&u)[R], ConstD t,
-                                             int d) {
-    double ck[14];
-#pragma unroll
-    for (int j = 0; j < 14; ++j) ck[j] = t[j];
-    const double c1 = t[14 - d];
-#pragma unroll
-    for (int r = 0; r < R; ++r) p[r] = fma_sc(ck[0], u[r], c1);
-#pragma unroll
-    for (int j = 2; j <= 13; ++j) {
-        if (j >= 15 - kChainD0 || d >= 15 - j) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck[j]);
-        }
-    }
-}
-// per-degree form: degree D's own chain from its table row (compile-time steps)
-template <int R, int D>
-__device__ __forceinline__ void horner_row(double (&p)[R], const double (&u)[R], ConstD t) {
-    const double top = t[0], c1 = t[14 - D];
-#pragma unroll
-    for (int r = 0; r < R; ++r) p[r] = fma_sc(top, u[r], c1);
-#pragma unroll
-    for (int j = 15 - D; j <= 13; ++j) {
-        const double ck = t[j];
-#pragma unroll
-        for (int r = 0; r < R; ++r) p[r] = fma_sc(p[r], u[r], ck);
-    }
-}
-// the wave's degree: the shortest whose interval holds every active lane's largest x4 (um);
-// a binary search of wave votes over kReluChainX (three per ReLU site)
-__device__ __forceinline__ int chain_degree(double um) {
-    static_assert(kChainRows == 8, "the search below covers degrees 6..13");
-    auto all = [&](int r) { return __all(um <= 4.0 * kReluChainX[r]); };
-    if (all(3)) {                                  // x <= X(9)
-        if (all(1)) return all(0) ? 6 : 7;
-        return all(2) ? 8 : 9;
-    }
-    if (all(5)) return all(4) ? 10 : 11;
-    return all(6) ? 12 : 13;
-}
-template <int R, int D = kChainD0>
-__device__ __forceinline__ void horner_pick(double (&p)[R], const double (&u)[R], ConstD tab,
-                                            int d) {
-    if constexpr (D == 13) {
-        horner_row<R, 13>(p, u, tab + (13 - kChainD0) * 14);
-    } else {
-        if (d == D)
-            horner_row<R, D>(p, u, tab + (D - kChainD0) * 14);
-        else
-            horner_pick<R, D + 1>(p, u, tab, d);
-    }
-}
-#endif
 // AD: 0 the full polynomial; 1 the range-adaptive choice, uniform over the wave (its lanes
-// hold one pair); 2 the choice per pair segment: `seg` is the mask of this wave's lanes that
-// hold the same pair as this lane (multi-pair stages, CGP_RELU_ADAPT_MP), so a pair's
-// polynomial depends on its own pixels only and a wave whose pairs disagree runs each
-// chosen polynomial under its lanes' exec mask
+// hold the same items of one pair in every workgroup); 2 the choice per vote group: `seg` is
+// the mask of this wave's lanes in this lane's vote group (multi-pair stages: a fixed set
+// of the pair's items, netfuse.hip vote_lanes), so a pair's polynomial depends on its own
+// pixels only and a wave whose groups disagree runs each chosen polynomial under its lanes'
+// exec mask
 template <int R, bool QIN, int AD = 0>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
                                          const double (&v2)[R], const PolyTab& tab,
@@ -473,53 +341,29 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         const double sq4 = m * __builtin_fma(-m, h, 3.0);
         sx[r] = (st[r] * u[r]) * sq4;
     }
-#if CGP_RELU_ADAPT
-    if constexpr (AD == 2) {
-        double um = u[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
-        const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
-        auto all_seg = [&](bool pred) { return (__ballot(pred) & seg) == ex; };
-        if (all_seg(um <= 4.0 * kReluAdaptX0)) {
-            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
-        } else if (all_seg(um <= 4.0 * kReluAdaptX1)) {
-            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
-        } else if (all_seg(um <= 4.0 * kReluAdaptX2)) {
-            horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
-        } else {
-            horner_q<R, kReluPolyDegD>(p, u, tab.dq);
-        }
-    } else if constexpr (AD == 1) {
-        // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
+    if constexpr (AD != 0) {
+        // the largest x4 = 4x of the lane's pixels; the group takes the shortest polynomial
         // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
-#if CGP_RELU_CHAIN || CGP_RELU_FINE
-        static_assert(kReluPolyDegD == 13, "the per-degree rows end in the degree-13 polynomial");
-        const int d = chain_degree(um);
-#if CGP_RELU_CHAIN
-        horner_chain<R>(p, u, tab.ch + (d - kChainD0) * 14, d);
-#else
-        horner_pick<R>(p, u, tab.ch, d);
-#endif
-#else
-        if (__all(um <= 4.0 * kReluAdaptX0)) {
+        const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
+        auto all = [&](bool pred) {
+            if constexpr (AD == 1) return __all(pred) != 0;
+            else return (__ballot(pred) & seg) == ex;
+        };
+        if (all(um <= 4.0 * kReluAdaptX0)) {
             horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
-        } else if (__all(um <= 4.0 * kReluAdaptX1)) {
+        } else if (all(um <= 4.0 * kReluAdaptX1)) {
             horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
-        } else if (__all(um <= 4.0 * kReluAdaptX2)) {
+        } else if (all(um <= 4.0 * kReluAdaptX2)) {
             horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
         } else {
             horner_q<R, kReluPolyDegD>(p, u, tab.dq);
         }
-#endif
     } else {
         horner_q<R, kReluPolyDegD>(p, u, tab.dq);
     }
-#else
-    horner_q<R, kReluPolyDegD>(p, u, tab.dq);
-#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = __builtin_fma(sx[r], p[r], c[r] + __builtin_fabs(c[r]));
 }
@@ -528,9 +372,6 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
 // exactly relu_fast's IEEE operations in the same order, so the packed form is
 // bit-identical to the scalar one; only min/max/abs and the rsq estimates stay scalar (no
 // packed form).  An odd R leaves one pixel on the scalar path.
-#ifndef CGP_F32_PACKED
-#define CGP_F32_PACKED 1
-#endif
 typedef float cgp_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cgp_f2 relu_fast2(cgp_f2 c, cgp_f2 v1, cgp_f2 v2) {
     const cgp_f2 t = __builtin_elementwise_fma(v1, v2, cgp_f2(K<float>::tiny));
@@ -603,13 +444,11 @@ __device__ __forceinline__ void relu_poly_f(const float (&P)[D + 1], float (&c)[
         c[R - 1] = __builtin_fmaf(ms, p, hs);
     }
 }
-// AD (one-pair code, CGP_RELU_ADAPT): the shortest float polynomial whose interval holds
-// every active lane's pixels of the wave (kReluAdaptF*: degrees 3 / 5 on x <= 1/8 / 3/8
-// at the degree-6 fit's bound)
-template <int R, bool AD = false>
+// R fp32 ReLUs: packed pairs + an odd scalar pixel through the degree-6 polynomial (its
+// range-adaptive form measured neutral: the fp32 kernel is latency bound)
+template <int R>
 __device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],
-                                            const float (&v2)[R], const PolyTab& tab) {
-#if CGP_F32_PACKED
+                                            const float (&v2)[R], const PolyTab&) {
     cgp_f2 x2[R / 2 + 1], m2[R / 2 + 1], h2[R / 2 + 1];
     float xs = 0.0f, ms = 0.0f, hs = 0.0f;
 #pragma unroll
@@ -617,26 +456,7 @@ __device__ __forceinline__ void relu_fast_n(float (&c)[R], const float (&v1)[R],
         relu_prep2(cgp_f2{c[2 * q], c[2 * q + 1]}, cgp_f2{v1[2 * q], v1[2 * q + 1]},
                    cgp_f2{v2[2 * q], v2[2 * q + 1]}, x2[q], m2[q], h2[q]);
     if constexpr (R % 2) relu_prep1(c[R - 1], v1[R - 1], v2[R - 1], xs, ms, hs);
-#if CGP_RELU_ADAPT
-    if constexpr (AD) {
-        float xmax = (R % 2) ? xs : 0.0f;
-#pragma unroll
-        for (int q = 0; q < R / 2; ++q) xmax = __builtin_fmaxf(xmax, __builtin_fmaxf(x2[q].x, x2[q].y));
-        if (__all(xmax <= kReluAdaptFX0)) {
-            relu_poly_f<R, kReluAdaptFDeg0>(kReluAdaptFP0, c, x2, m2, h2, xs, ms, hs);
-        } else if (__all(xmax <= kReluAdaptFX1)) {
-            relu_poly_f<R, kReluAdaptFDeg1>(kReluAdaptFP1, c, x2, m2, h2, xs, ms, hs);
-        } else {
-            relu_poly_f<R, kReluPolyDegF>(kReluPolyF, c, x2, m2, h2, xs, ms, hs);
-        }
-        return;
-    }
-#endif
     relu_poly_f<R, kReluPolyDegF>(kReluPolyF, c, x2, m2, h2, xs, ms, hs);
-#else
-#pragma unroll
-    for (int r = 0; r < R; ++r) c[r] = relu_fast(c[r], v1[r], v2[r], tab);
-#endif
 }
 
 template <typename T>

@@ -1278,6 +1278,9 @@ struct BlasDev {
     int64_t* dinfo = nullptr;
     int64_t* dinfos = nullptr;     // one info word per diagonal block (chol_blocked)
     int64_t ninfos = 0;
+    hipEvent_t ev[4] = {};         // cgp_chol_solve_f64 phase marks (created on first solve)
+    double phase_ms[3] = {};       // jitter, factor, potrs of the last solve
+    bool timed = false;
 };
 std::mutex g_blas_reg_mu;
 std::map<int, BlasDev*> g_blas;
@@ -1533,12 +1536,25 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
     std::lock_guard<std::mutex> lk(b->mu);
     rocblas_handle h = b->h;
     CGP_BLAS(rocblas_set_stream(h, s));
+    if (!b->ev[0]) {
+        int dev = 0, cur = 0;
+        CGP_HIP(stream_device(s, &dev));
+        CGP_HIP(hipGetDevice(&cur));
+        CGP_HIP(hipSetDevice(dev));
+        hipError_t e = hipSuccess;
+        for (int q = 0; q < 4 && e == hipSuccess; ++q) e = hipEventCreate(&b->ev[q]);
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) return fail(CGP_EHIP, "chol: events: %s", hipGetErrorString(e));
+    }
+    b->timed = false;
+    CGP_HIP(hipEventRecord(b->ev[0], s));
     if (jitter != 0.0) {
         hipLaunchKernelGGL(diag_add_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, k,
                            (long long)n, (long long)ldk, jitter);
         rc = check_launch("diag_add_kernel");
         if (rc) return rc;
     }
+    CGP_HIP(hipEventRecord(b->ev[1], s));
     // row-major upper triangle == column-major lower triangle
     int64_t hinfo = -1;
     const int64_t nb = chol_nb();
@@ -1550,11 +1566,29 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
         CGP_HIP(hipMemcpyAsync(&hinfo, b->dinfo, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         CGP_HIP(hipStreamSynchronize(s));
     }
+    CGP_HIP(hipEventRecord(b->ev[2], s));
     *info = hinfo;
-    if (hinfo == 0) {
+    if (hinfo == 0)
         CGP_BLAS(rocsolver_dpotrs_64(h, rocblas_fill_lower, n, nrhs, k, ldk, bt, ldb));
-        CGP_HIP(hipStreamSynchronize(s));
+    CGP_HIP(hipEventRecord(b->ev[3], s));
+    CGP_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < 3; ++q) {
+        float ms = 0.f;
+        CGP_HIP(hipEventElapsedTime(&ms, b->ev[q], b->ev[q + 1]));
+        b->phase_ms[q] = ms;
     }
+    b->timed = true;
+    return CGP_OK;
+}
+
+int cgp_chol_last_phases(void* stream, double* ms) {
+    if (!ms) return fail(CGP_EINVAL, "chol_last_phases: NULL argument");
+    BlasDev* b = nullptr;
+    const int rc = blas_dev(as_stream(stream), &b);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!b->timed) return fail(CGP_EINVAL, "chol_last_phases: no solve on this device yet");
+    for (int q = 0; q < 3; ++q) ms[q] = b->phase_ms[q];
     return CGP_OK;
 }
 

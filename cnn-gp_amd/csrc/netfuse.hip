@@ -32,26 +32,19 @@ using namespace cgp;
 
 namespace {
 
-#ifndef CGP_NET_NT
-#define CGP_NET_NT 128
-#endif
-constexpr int kNT = CGP_NET_NT;  // threads per workgroup (one pair): two waves
+constexpr int kNT = 128;  // threads per workgroup (one pair): two waves
 // threads of a workgroup carrying NP pairs: NP == 2 is two one-pair halves on four waves
 // (units u and u + 1, the same image i: the i-side variance loads of the halves meet in
 // L1 and each barrier serves both pairs; net_kernel); the small-map stages pack 4 / 16
-// pairs on two waves.  Ops only ever run on one half (NP = 1) or on NP = 4 / 16.
-#ifndef CGP_NET_SPLIT
-#define CGP_NET_SPLIT 2   // one-pair slices of a "2-pair" workgroup (A/B builds: 4)
-#endif
+// pairs on two waves.  Ops only ever run on one half (NP = 1) or on NP = 4 / 16.  (Four
+// one-pair slices on 512 threads measured -15% fp64: LDS then admits 2 workgroups per CU.)
+constexpr int kSplit = 2;
 template <int NP>
-constexpr int kNTof = NP == 2 ? CGP_NET_SPLIT * kNT : kNT;
+constexpr int kNTof = NP == 2 ? kSplit * kNT : kNT;
 // pair units a workgroup takes per step of the walk
 template <int NP>
-constexpr int kUnitsOf = NP == 2 ? CGP_NET_SPLIT : NP;
-#ifndef CGP_NET_STL
-#define CGP_NET_STL 3
-#endif
-constexpr int kSTL = CGP_NET_STL;   // log2(kST)
+constexpr int kUnitsOf = NP == 2 ? kSplit : NP;
+constexpr int kSTL = 3;             // log2(kST) (16² / 32² supertiles measured ±0.7%)
 constexpr int kST = 1 << kSTL;      // supertile edge: pairs are walked in 8x8 (i, j) blocks
 constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
 
@@ -94,11 +87,8 @@ struct NG {
     static constexpr int NG3 = HO / R3, NV = NG3 * WO, KV = (NP * NV + NT - 1) / NT;
     static constexpr int NZ = (HSR - NVR) * WO;                // zero cells of hs
     // windows of at most 3 taps (the ResNets' 3x3 convs) run in one pass straight from the
-    // source slot: no row-sum scratch, so a smaller arena (CGP_NET_DIRECT=0: separable)
-#ifndef CGP_NET_DIRECT
-#define CGP_NET_DIRECT 1
-#endif
-    static constexpr bool DIRECT = CGP_NET_DIRECT && !POINT && !REDUCE && TAPS <= 3;
+    // source slot: no row-sum scratch, so a smaller arena
+    static constexpr bool DIRECT = !POINT && !REDUCE && TAPS <= 3;
     static constexpr int HS_ELEMS = (POINT || REDUCE || DIRECT) ? 2 : HSR * WO;
 };
 
@@ -190,54 +180,24 @@ __device__ __forceinline__ void win_sums(const T (&w)[(R - 1) * S + TAPS], T (&o
 
 // threadIdx.x through an opaque move: per-thread index math of one op is then recomputed
 // inside the op instead of being hoisted out of the pair loop, where it would hold
-// registers for every geometry at once
+// registers for every geometry at once (hoisted: -1% fp64, scratch spills in the head
+// programs)
 // (thread index within its 128-thread half: a two-pair workgroup runs one pair per half)
-#ifndef CGP_NET_OPAQUE_TID
-#define CGP_NET_OPAQUE_TID 1
-#endif
 __device__ __forceinline__ int opaque_tid() {
     static_assert(kNT == 128, "opaque_tid masks to 128-thread halves");
-#if CGP_NET_OPAQUE_TID
     int t;
     asm volatile("v_and_b32 %0, 0x7f, %1" : "=v"(t) : "v"((int)threadIdx.x));
     return t;
-#else
-    return (int)(threadIdx.x & 127u);
-#endif
-}
-
-// An LDS element index folded into one register: ds_read2_b64's offsets reach 255 doubles
-// (2040 bytes), so a window whose constant base (the slot origin) lies further out gets one
-// v_add per read pair; with the base added into the index once, behind an empty asm the
-// compiler cannot see through, the window's reads keep their small immediates
-// (CGP_NET_LDS_BASE, A/B option)
-#ifndef CGP_NET_LDS_BASE
-#define CGP_NET_LDS_BASE 0
-#endif
-__device__ __forceinline__ int lds_index(int e) {
-#if CGP_NET_LDS_BASE
-    asm("" : "+v"(e));
-#endif
-    return e;
 }
 
 // a / d for a >= 0 as an unsigned division (a constant d costs a mul-hi and a shift; the
 // signed form needs three more fix-up ops)
 __device__ __forceinline__ int udiv(int a, int d) { return (int)((unsigned)a / (unsigned)d); }
 
-// the op table through the constant address space: the kernel never writes it, so its
-// fields load with scalar loads into SGPRs (a generic pointer gets per-lane vector loads
-// because stores to the output could alias it)
-#ifndef CGP_NET_SCALAR_OPS
-#define CGP_NET_SCALAR_OPS 0
-#endif
-#if CGP_NET_SCALAR_OPS
-typedef const __attribute__((address_space(4))) cgp_net_op* OpsC;
-#else
-typedef const cgp_net_op* OpsC;
-#endif
-__device__ __forceinline__ OpsC ops_c(const cgp_net_op* p) { return (OpsC)p; }
-__device__ __forceinline__ cgp_net_op load_op(OpsC r) {
+// the op table through a generic pointer: per-lane vector loads (the constant address
+// space's scalar loads measured -7% on ConvNet: SMEM returns count in lgkmcnt, so every
+// LDS wait also drains them)
+__device__ __forceinline__ cgp_net_op load_op(const cgp_net_op* r) {
     cgp_net_op o;
     o.kind = r->kind;
     o.code = r->code;
@@ -285,7 +245,7 @@ struct NetP {
     T* __restrict__ out;
     const T* __restrict__ kdiag;
     const cgp_net_op* __restrict__ ops;
-    unsigned long long* work;   // per-XCD unit counters (CGP_NET_DYN), zeroed per launch
+    unsigned long long* work;   // per-XCD unit counters, zeroed per launch
     long long ldo, units, ubeg, uend;
     unsigned n1, n2, nbi, nbj;
     int nops, channels, hw_in, same, final_slot, hs, lds_elems, exact, final_stage, part;
@@ -325,13 +285,10 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
 template <typename T, bool EX>
 constexpr bool kQuarter = !EX && sizeof(T) == 8;
 
-// the fp32 closed form's adaptive polynomial measured neutral (the fp32 kernel is bound by
-// its per-op latency chain, not by issue; profiles/r3/ab_r3f_relu_adapt_f32.log): off
-#ifndef CGP_RELU_ADAPT_F32
-#define CGP_RELU_ADAPT_F32 0
-#endif
-// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4; AD: the caller's
-// waves hold one pair's pixels, so the fp64 form may take the range-adaptive polynomial)
+// R ReLUs in place: v[k] = relu(v[k], u1[k], u2[k]) (QIN: v holds c/4; AD: the fp64 form
+// may take the range-adaptive polynomial, see relu_q_n).  The fp32 closed form keeps its
+// full polynomial: its adaptive form measured neutral (the fp32 kernel is bound by its
+// per-op latency chain, not by issue; profiles/r3/ab_r3f_relu_adapt_f32.log)
 template <bool EXACT, bool QIN, typename T, int R, int AD = 0>
 __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2)[R],
                                        const PolyTab& tab, unsigned long long seg = ~0ull) {
@@ -341,7 +298,7 @@ __device__ __forceinline__ void relu_n(T (&v)[R], const T (&u1)[R], const T (&u2
     } else if constexpr (sizeof(T) == 8) {
         relu_q_n<R, QIN, AD>(v, u1, u2, tab, seg);
     } else {
-        relu_fast_n<R, AD == 1 && CGP_RELU_ADAPT_F32>(v, u1, u2, tab);
+        relu_fast_n<R>(v, u1, u2, tab);
     }
 }
 
@@ -448,74 +405,70 @@ __device__ __forceinline__ VarSrc<T> var_src(const cgp_net_op& op, unsigned i, u
 // ---- CGP_NET_CONV -------------------------------------------------------------------
 // G::NP pairs: item it of a pass belongs to pair q = it / (items per pair) and works on
 // that pair's LDS arena (q · lds_elems) and variance maps.
-// Range-adaptive ReLU in a conv epilogue: one-pair code votes over the wave (AD 1);
-// multi-pair stages vote per pair segment of the wave (AD 2; CGP_RELU_ADAPT_MP, default on
-// since round 3: +0.5% mnist_as_tf, +0.8% cifar10, profiles/r3/ab_r3k_chain_undef_ldsb_mp.log;
-// =0 keeps the full polynomial there).
-#ifndef CGP_RELU_ADAPT_MP
-#define CGP_RELU_ADAPT_MP 1
-#endif
+// Range-adaptive ReLU in a conv epilogue (relu_q_n): one-pair code votes over the wave
+// (AD 1: both waves of a pair hold the same items of it in every workgroup); multi-pair
+// stages vote per vote group (AD 2, below).
 template <int NP>
-constexpr int kAdaptOf = NP == 1 ? 1 : (CGP_RELU_ADAPT_MP ? 2 : 0);
-#ifndef CGP_NET_RES_UNDEF
-#define CGP_NET_RES_UNDEF 0
-#endif
-// Wave priority (CGP_NET_PRIO, default 2): a conv raises its waves' issue priority
-// (s_setprio) while it sends its variance loads and window reads and drops it for the
-// arithmetic epilogue, so the memory requests of a wave entering an op go out ahead of the
-// other waves' long ALU runs and their latency overlaps that work.  Measured (one B = 1024
-// Kxz tile, profiles/r3/ab_r3u_prio.log): ConvNet +4.5-5%, Residual +4-5%, mnist_as_tf +3%
-// (its 28x28 head; the multi-pair stages do not move), but the cifar10 head (32x32 maps,
-// four waves per SIMD) -3%: applied to maps of at most CGP_NET_PRIO_MAXHW pixels.
-#ifndef CGP_NET_PRIO
-#define CGP_NET_PRIO 2
-#endif
-#ifndef CGP_NET_PRIO_MP      // also in the multi-pair (4 / 16 pairs) stages
-#define CGP_NET_PRIO_MP 1
-#endif
-#ifndef CGP_NET_PRIO_MAXHW
-#define CGP_NET_PRIO_MAXHW (28 * 28)
-#endif
+constexpr int kAdaptOf = NP == 1 ? 1 : 2;
+// Wave priority: a conv raises its waves' issue priority (s_setprio 2) while it sends its
+// variance loads and window reads and drops it for the arithmetic epilogue, so the memory
+// requests of a wave entering an op go out ahead of the other waves' long ALU runs and
+// their latency overlaps that work.  Measured (one B = 1024 Kxz tile,
+// profiles/r3/ab_r3u_prio.log): ConvNet +4.5-5%, Residual +4-5%, mnist_as_tf +3% (its 28x28
+// head; the multi-pair stages do not move), but the cifar10 head (32x32 maps, four waves
+// per SIMD) -3%: applied to maps of at most 28x28 pixels.  Priority 1 / 2 / 3 measure the
+// same; raised over the variance loads only, or the window reads only, it loses half or
+// more of the gain (profiles/r3/ab_r3x_prio_span.log); around the elementwise ops' loads
+// it adds nothing.
+constexpr int kPrio = 2;
+constexpr int kPrioMaxHW = 28 * 28;
 template <int NP, int HW>
-constexpr bool kPrioOn = CGP_NET_PRIO > 0 && (NP == 1 || CGP_NET_PRIO_MP) &&
-                         HW <= CGP_NET_PRIO_MAXHW;
+constexpr bool kPrioOn = HW <= kPrioMaxHW;
 template <int NP, int HW>
 __device__ __forceinline__ void prio_mem() {
-    if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(CGP_NET_PRIO);
+    if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(kPrio);
 }
 template <int NP, int HW>
 __device__ __forceinline__ void prio_alu() {
     if constexpr (kPrioOn<NP, HW>) __builtin_amdgcn_s_setprio(0);
 }
-// CGP_NET_PRIO_SPAN (A/B): 0 = the variance loads and the window reads (default), 1 = the
-// variance loads only (dropped before the window reads: loses most of the gain), 2 = the
-// window reads only (raised after the variance loads)
-#ifndef CGP_NET_PRIO_SPAN
-#define CGP_NET_PRIO_SPAN 0
-#endif
-template <int NP, int HW>
-__device__ __forceinline__ void prio_before_loads() {
-    if constexpr (CGP_NET_PRIO_SPAN != 2) prio_mem<NP, HW>();
-}
-template <int NP, int HW>
-__device__ __forceinline__ void prio_after_loads() {
-    if constexpr (CGP_NET_PRIO_SPAN == 1) prio_alu<NP, HW>();
-    if constexpr (CGP_NET_PRIO_SPAN == 2) prio_mem<NP, HW>();
-}
-// the same around the loads of the elementwise ops (moments, standalone ReLU, LINEAR):
-// A/B option CGP_NET_PRIO_ELEM
-#ifndef CGP_NET_PRIO_ELEM
-#define CGP_NET_PRIO_ELEM 0
-#endif
-// lanes of this wave whose item belongs to the same pair as item `it` (items of pair q
-// are [q·per, (q+1)·per); item it sits on lane it % 64 of its wave)
-__device__ __forceinline__ unsigned long long pair_lanes(int it, int per) {
-    const int wb = it & ~63, q = udiv(it, per);
-    int lo = q * per - wb, hi = (q + 1) * per - wb;
-    lo = lo < 0 ? 0 : lo;
-    hi = hi > 64 ? 64 : hi;
-    const unsigned long long top = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-    return top & ~((1ull << lo) - 1ull);
+// Vote groups of a multi-pair stage (AD 2).  Items of pair q are [q·PER, (q+1)·PER) and
+// item it runs on lane it % 64 of wave it / 64, so which items of a pair share a wave
+// depends on the pair's slot q in the workgroup — a vote over "this pair's lanes of this
+// wave" would make a pair's polynomial choice depend on its slot, i.e. on its place in the
+// tile (1-ulp differences between a tile and a single-pair forward, found at round 4).
+// Instead every pair's items are cut at the same local offsets: every offset at which a
+// wave boundary can fall for SOME slot, {64k mod PER}.  A group then never straddles a
+// wave, and it is the same set of the pair's pixels in every slot, so a pair's result
+// depends on its own pixels only.
+template <int PER, int NPR>
+struct VoteCuts {
+    int n = 0;
+    int at[64] = {};
+    constexpr VoteCuts() {
+        for (int off = 1; off < PER && n < 64; ++off) {
+            bool cut = false;
+            for (int k = 1; 64 * k < NPR * PER; ++k) cut = cut || (64 * k) % PER == off;
+            if (cut) at[n++] = off;
+        }
+    }
+};
+// the lanes of this wave in item it's vote group (a mask over the wave's 64 lanes)
+template <int PER, int NPR>
+__device__ __forceinline__ unsigned long long vote_lanes(int it) {
+    constexpr VoteCuts<PER, NPR> cuts{};
+    const int wb = it & ~63, q = udiv(it, PER), l = it - q * PER;
+    int lo = 0, hi = PER;
+#pragma unroll
+    for (int k = 0; k < cuts.n; ++k) {
+        if (cuts.at[k] <= l) lo = cuts.at[k];
+        if (cuts.at[k] > l && cuts.at[k] < hi) hi = cuts.at[k];
+    }
+    int a = q * PER + lo - wb, b = q * PER + hi - wb;
+    a = a < 0 ? 0 : a;
+    b = b > 64 ? 64 : b;
+    const unsigned long long top = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+    return top & ~((1ull << a) - 1ull);
 }
 template <typename T, bool EX, bool DU, class G>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
@@ -527,7 +480,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
-    prio_before_loads<NP, G::HW>();
+    prio_mem<NP, G::HW>();
     const VarSrc<T> vs0 = var_src<T, NP == 1>(op, pr.i, pr.j, G::HOWO);   // NP == 1
     auto vs_of = [&](int q) {
         if constexpr (NP == 1) {
@@ -644,7 +597,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 u2[kv][k] = vs.on ? vs.ldy(px0, k * G::WO) : T(1);
             }
         }
-        prio_after_loads<NP, G::HW>();
         // outputs that land on the source (in place, or dst2 on the source) are stored
         // after every item has read its window
         const int s_lo = op.src - wsi, s_hi = op.src + G::H * wsi;
@@ -653,14 +605,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         };
         const bool hazard = hits(op.dst) || (DU && hits(op.dst2));
         T res[G::KV][G::R3];
-#if CGP_NET_RES_UNDEF
-        // items past NVT never read res: an empty asm defines it without an instruction
-        // (left undefined, the compiler zeroes every entry on that path: R3 moves per op)
-#pragma unroll
-        for (int kv = 0; kv < G::KV; ++kv)
-#pragma unroll
-            for (int k = 0; k < G::R3; ++k) asm("" : "=v"(res[kv][k]));
-#endif
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * G::NT;
@@ -707,7 +651,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                 }
                 net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, res[kv], at, ok, u1[kv],
                                                         u2[kv], tab,
-                                                        NP == 1 ? ~0ull : pair_lanes(it, G::NV));
+                                                        NP == 1 ? ~0ull : vote_lanes<G::NV, NP>(it));
             }
         }
     } else {
@@ -736,7 +680,6 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 #pragma unroll
                 for (int k = 0; k < G::R3; ++k) u1[kv][k] = u2[kv][k] = T(1);
         }
-        prio_after_loads<NP, G::HW>();
         // row pass: hs[q][c] = Σ_t in[q + OFF][c·S + OFF + t]
 #pragma unroll
         for (int kh = 0; kh < G::KH; ++kh) {
@@ -744,8 +687,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NHT % G::NT == 0 || it < NHT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NH), l = it - q * G::NH;
                 const int qi = udiv(l, G::NG2), g2 = l - qi * G::NG2;
-                const T* row = lds + lds_index(op.src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
-                                               g2 * G::R2 * G::S + G::OFF);
+                const T* row = lds + op.src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
+                               g2 * G::R2 * G::S + G::OFF;
                 T win[G::WIN2];
 #pragma unroll
                 for (int t = 0; t < G::WIN2; ++t) win[t] = row[t];
@@ -779,7 +722,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
-                const T* col = lds + lds_index(p.hs + q * arena + g3 * G::R3 * G::S * G::WO + c);
+                const T* col = lds + p.hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
@@ -800,7 +743,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     ok[k] = true;
                 }
                 net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, v, at, ok, u1[kv], u2[kv], tab,
-                                                        NP == 1 ? ~0ull : pair_lanes(it, G::NV));
+                                                        NP == 1 ? ~0ull : vote_lanes<G::NV, NP>(it));
             }
         }
     }
@@ -836,8 +779,6 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     const int n = NP * hw;
     // waves with no pixel in this pass skip the ReLUs (uniform per wave)
     const bool live = base + (tid & ~63) < n;
-    constexpr bool kPE = CGP_NET_PRIO_ELEM && kPrioOn<NP, (W_ > 0 ? W_ * W_ : 0)>;
-    if constexpr (kPE) prio_mem<NP, 0>();
     T a[KE], u1[KE], u2[KE];
     int at[KE];
     bool ok[KE];
@@ -871,7 +812,6 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
             a[k] = T(op.weight) * lds[op.src + at[k]] + T(op.bias) * lds[op.add + at[k]];
         }
     }
-    if constexpr (kPE) prio_alu<NP, 0>();
     if constexpr (KIND == CGP_NET_MOMENTS) {
         // the channel mean (x / 1 == x: a uniform branch, so one-channel inputs run no
         // division at all)
@@ -1108,7 +1048,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
     constexpr ProgInfo I = kProgs[PID];
     if constexpr (K < I.nops) {
         constexpr ProgOp o = kProgOps[I.first + K];
-        const auto& rt = ops_c(p.ops)[K];
+        const auto& rt = p.ops[K];
         cgp_net_op op;
         op.kind = o.kind;
         op.code = o.code;
@@ -1184,15 +1124,6 @@ int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_ele
 // registers for more waves than that only forces spills; net_launch picks WPE from the
 // LDS footprint (net_wpe).  NP: pairs per workgroup (1; 2 on four waves, sharing image i;
 // 4 / 16 for small-map stages).
-#ifndef CGP_NET_DYN
-#define CGP_NET_DYN 1
-#endif
-#ifndef CGP_NET_XCD_PROBE
-#define CGP_NET_XCD_PROBE 0
-#endif
-#if CGP_NET_XCD_PROBE
-__device__ unsigned long long g_exit_clock[1 << 16];
-#endif
 // PID >= 0: compiled program PID instead of the op-record interpreter.
 template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
 __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
@@ -1206,12 +1137,11 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
     // contiguous run of supertiles and its L2 holds the images/variances they share.
     // Ranges and groups are whole multiples of NP units.
-    const unsigned g8 = gridDim.x / 8, xcd = blockIdx.x % 8, l = blockIdx.x / 8;
+    const unsigned xcd = blockIdx.x % 8;
     const long long span = p.uend - p.ubeg;
     const long long per = ((span + 7) / 8 + UN - 1) / UN * UN;
     const long long beg = p.ubeg + (long long)xcd * per;
     const long long end = beg + per < p.uend ? beg + per : p.uend;
-#if CGP_NET_DYN
     // the XCD's workgroups take its units in order from one counter, so the pairs in
     // flight on an XCD stay one contiguous window (a few supertiles) whose images and
     // variance maps its L2 holds; a static stride lets workgroups drift apart and the
@@ -1221,8 +1151,6 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     __shared__ long long next_u[2];
     int adv = 0;
     unsigned long long* ctr = p.work + xcd;
-    (void)g8;
-    (void)l;
     unsigned long long grab = 0;   // thread 0: the counter value fetched one pair ahead
     if (tid == 0) grab = atomicAdd(ctr, 1ull);
     auto advance = [&]() {
@@ -1234,9 +1162,6 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     };
     for (long long u = advance(); u < end; u = advance()) {
         if (tid == 0) grab = atomicAdd(ctr, 1ull);
-#else
-    for (long long u = beg + (long long)l * UN; u < end; u += (long long)g8 * UN) {
-#endif
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
@@ -1278,7 +1203,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             const int ht = tid & (kNT - 1);
             if constexpr (PID < 0) {
                 for (int k = 0; k < p.nops; ++k) {
-                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
+                    const cgp_net_op op = load_op(p.ops + k);
                     net_op<T, EX, DU, 1>(lh, op, p, ph, ht);
                     lds_barrier();
                 }
@@ -1318,7 +1243,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             }
             if constexpr (PID < 0) {
                 for (int k = 0; k < p.nops; ++k) {
-                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
+                    const cgp_net_op op = load_op(p.ops + k);
                     net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
                     lds_barrier();
                 }
@@ -1348,11 +1273,6 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
         }
         lds_barrier();
     }
-#if CGP_NET_XCD_PROBE
-    // A/B builds: each workgroup's exit time (s_memrealtime, 100 MHz) for the per-XCD
-    // balance probe (tools/xcd_probe.py)
-    if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) g_exit_clock[blockIdx.x] = wall_clock64();
-#endif
 }
 
 // waves per SIMD the LDS footprint of a workgroup allows (`waves` waves per workgroup,
@@ -1362,17 +1282,11 @@ constexpr int net_wpe(long long lds_bytes, int cap = 5, int waves = kNT / 64) {
     const long long w = wg * waves / 4;
     return w < 3 ? 3 : (w > cap ? cap : (int)w);
 }
-#ifndef CGP_NET_PROG_WPE_F32
-#define CGP_NET_PROG_WPE_F32 0   // > 0: fp32 programs' register target from their LDS, capped
-#endif
-#ifndef CGP_NET_PROG_WPE_MAX
-#define CGP_NET_PROG_WPE_MAX 5
-#endif
-// register target cap of the multi-pair (4 / 16 pairs) fp64 stage programs (A/B knob: the
-// per-segment adaptive ReLU spills 13 VGPRs in mnist_as_tf's 14x14 stage at 5)
-#ifndef CGP_NET_PROG_WPE_MP
-#define CGP_NET_PROG_WPE_MP CGP_NET_PROG_WPE_MAX
-#endif
+// register target cap of the fp64 compiled programs (6 waves per SIMD: -1…-2% on the
+// ResNets; the multi-pair stages at 4: slower than their 13 spilled VGPRs at 5,
+// profiles/r3/ab_r3r_mp_wpe.log); the fp32 programs keep the plain 4 / 5 targets (from
+// their LDS capped at 6 / 8: within ±1% except Residual +5%)
+constexpr int kProgWpeMax = 5;
 
 // the instantiation for (EX, DU, pairs, LDS footprint of the workgroup): the fp64 closed
 // form — the production path — has a register target per occupancy level; fp32 one per
@@ -1428,13 +1342,8 @@ const void* prog_fn_one() {
     } else {
         constexpr long long bytes =
             (long long)I.lds_elems * (long long)sizeof(T) * kUnitsOf<I.pairs>;
-        constexpr int wpe = sizeof(T) == 8
-                                ? net_wpe(bytes, I.pairs > 2 ? CGP_NET_PROG_WPE_MP
-                                                             : CGP_NET_PROG_WPE_MAX,
-                                          kNTof<I.pairs> / 64)
-                                : CGP_NET_PROG_WPE_F32 > 0
-                                      ? net_wpe(bytes, CGP_NET_PROG_WPE_F32, kNTof<I.pairs> / 64)
-                                      : (I.dual ? 4 : 5);
+        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes, kProgWpeMax, kNTof<I.pairs> / 64)
+                                           : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
 }
@@ -1667,12 +1576,6 @@ int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t 
                       lds_elems, itemsize);
 }
 
-#if CGP_NET_XCD_PROBE
-int cgp_net_probe_read(unsigned long long* host, int32_t n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_exit_clock), sizeof(unsigned long long) * n) ==
-                   hipSuccess ? 0 : CGP_EHIP;
-}
-#endif
 int cgp_net_f64(const cgp_net_args* args, void* stream) { return net_impl<double>(args, stream); }
 int cgp_net_f32(const cgp_net_args* args, void* stream) { return net_impl<float>(args, stream); }
 

@@ -194,6 +194,14 @@ int cgp_transpose_f64(const double* src, int64_t rows, int64_t cols, double* dst
 int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
                        int64_t ldb, double jitter, int64_t* info, void* stream);
 /*
+ * Phase times (ms, HIP events on the call's stream) of the last cgp_chol_solve_f64 on
+ * `stream`'s device: ms[0] = jitter (diag_add, classify_gp.py:30-36), ms[1] = the
+ * Cholesky factorisation, ms[2] = dpotrs (0 when the factorisation failed).  Lets a
+ * caller split the solve_system wall time of classify_gp.py:17-27 (no reference
+ * counterpart: the reference times nothing).  CGP_EINVAL before any solve on that device.
+ */
+int cgp_chol_last_phases(void* stream, double* ms);
+/*
  * Row-major C[m][n] = A[m][kdim] @ B[kdim][n] (fp64, rocBLAS) — the Kxz @ α product of
  * print_accuracy, classify_gp.py:39-42.
  */
@@ -379,8 +387,8 @@ int cgp_net_resolution(int32_t h, int32_t w);
  * pairs per workgroup (0 if it cannot run) */
 int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs);
 /* LDS arenas (one per pair unit) a workgroup of `pairs` pairs holds: `pairs`, except for
- * the two-pair head stage, whose workgroup holds CGP_NET_SPLIT one-pair slices (2 in the
- * default build).  A stage needs lds_bytes × cgp_net_units(pairs) <= 160 KB. */
+ * the two-pair head stage, whose workgroup holds two one-pair slices.  A stage needs
+ * lds_bytes × cgp_net_units(pairs) <= 160 KB. */
 int cgp_net_units(int32_t pairs);
 /* The compiled program (k > 0) whose op list equals ops[0, nops) (HOST memory) in every
  * field but weight, bias and the variance / state pointers, for `pairs` pairs per

@@ -22,6 +22,7 @@ False) (oracle parity at this geometry: tests/test_gpu_fullgeom.py), and the sol
 residual ‖Kxx·α − Y‖ / ‖Y‖ on a random subset of rows.
 """
 import argparse
+import datetime
 import importlib
 import json
 import os
@@ -62,7 +63,7 @@ def widen(t):
 
 def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spot=16,
               pred_var=False, rank=0, world=1, dev=None, group=None,
-              kernel_dtype=torch.float64):
+              kernel_dtype=torch.float64, stats_group=None):
     """Kxx (n) + rocSOLVER solve + Kxz (m × n) + predict on the device, through
     cnn_gp.pipeline.classify_distributed: with world > 1 every rank builds a row strip of
     Kxx (balanced by evaluated pairs), rank 0 receives the strips into the full matrix and
@@ -72,7 +73,9 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     kernel_dtype float32 runs the kernels the way the reference's own pipeline does
     (save_kernel.py:19-24: the float32 model on float32 images, K stored float32 by
     kernel_save_tools.py:21) and widens K to float64 for the solve (classify_gp.py:45-48);
-    the spot check then also reports the float32 entries against the float64 model."""
+    the spot check then also reports the float32 entries against the float64 model.
+    With world > 1 the result carries every rank's own phase times (``ranks``), gathered
+    over ``stats_group`` (e.g. a gloo side group; default the pipeline's group)."""
     from cnn_gp.gram import model_kern
     from cnn_gp.pipeline import classify_distributed
     dev = dev or torch.device("cuda", torch.cuda.current_device())
@@ -96,12 +99,18 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     def solve(K, Yd):
         # the residual rows of K before it is factored in place (K is symmetric, its
         # upper triangle is filled)
+        t = time.perf_counter()
         r = rows.to(K.device)
         saved["Krows"] = torch.where(torch.arange(n, device=K.device)[None, :] >= r[:, None],
                                      K[r], K[:, r].T)
-        return cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+        torch.cuda.synchronize(K.device)
+        saved["rows_s"] = time.perf_counter() - t
+        A = cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+        saved["phases"] = cnn_gp.solve_phases(K.device)
+        return A
 
     torch.cuda.reset_peak_memory_stats(dev)
+    times = {}
     t0 = time.perf_counter()
     with torch.no_grad():
         out = classify_distributed(model_kern(model), X, Z, Y, solve, cnn_gp.scores,
@@ -110,15 +119,32 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                    widen=widen if kd != torch.float64 else None,
                                    log=lambda msg: log(rank, msg),
                                    warm=lambda: cnn_gp.warm_up_solver(dev),
-                                   cast=cnn_gp.cast_into)
+                                   cast=cnn_gp.cast_into, rank_times=times)
     wall = time.perf_counter() - t0
+    ranks = [times]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, times, group=stats_group or group)
     if rank != 0:
         return None
     kxx_bytes = n * n * 8
     res.update({k: out[k] for k in ("kxx_s", "gather_kxx_s", "kxx_to_kxz_s", "predict_s",
                                     "total_s")})
+    ph = saved["phases"]
     res.update(solve_s=out["solve_s"], kxz_s_rank0=out["kxz_s_rank"],
                solve_tflops=round(n ** 3 / 3 / out["solve_s"] / 1e12, 2),
+               solve_split={"widen_s": out.get("widen_s", 0.0),
+                            "residual_rows_s": round(saved["rows_s"], 4),
+                            "jitter_s": round(ph["jitter_s"], 4),
+                            "factor_s": round(ph["factor_s"], 4),
+                            "potrs_s": round(ph["potrs_s"], 4),
+                            "rest_s": round(out["solve_s"] - out.get("widen_s", 0.0) -
+                                            saved["rows_s"] - sum(ph.values()), 4),
+                            "factor_tflops": round(n ** 3 / 3 / ph["factor_s"] / 1e12, 2),
+                            "note": "solve_s = widen (float32 K only) + the 8 residual rows "
+                                    "copied before K is factored in place + jitter + "
+                                    "Cholesky + dpotrs (HIP events inside "
+                                    "cgp_chol_solve_f64) + rest (Y/alpha transposes, host)"},
                kxx_pairs_per_s=round(n * (n - 1) / 2 / out["kxx_s"], 1),
                plan_kxx=out["plan_kxx"], plan_kxz=out["plan_kxz"],
                kxz_share=out["kxz_share"],
@@ -129,6 +155,8 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                                       kxx_bytes, 3))
     if world == 1:
         res["kxz_s"] = out["kxz_s_rank"]
+    else:
+        res["ranks"] = ranks
     K, A = out["K"], out["alpha"]
     # residual on 8 rows of the (jittered) system: ‖K·α − Y‖ / ‖Y‖
     Kr = saved["Krows"].double()
@@ -145,8 +173,10 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     with torch.no_grad():
         for k, a in enumerate(rows.tolist()):
             for b in torch.randint(0, n, (max(1, spot // 8),), generator=gs).tolist():
+                # the upper triangle holds pair (min, max): the kernel's own orientation
+                lo, hi = min(a, b), max(a, b)
                 ref = model(X[a:a + 1]).item() if a == b else \
-                    model(X[a:a + 1], X[b:b + 1], False, False).item()
+                    model(X[lo:lo + 1], X[hi:hi + 1], False, False).item()
                 worst = max(worst, abs(saved["Krows"][k, b].item() - ref) / abs(ref))
         if z1 > z0:
             Kz = out["Kxz_rows"]
@@ -207,7 +237,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        tmo = datetime.timedelta(seconds=float(os.environ.get("CGP_DIST_TIMEOUT_S", "300")))
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        dist.init_process_group("nccl", device_id=dev, timeout=tmo)
     res = fullscale(args.config, args.n, args.m, args.tile, args.jitter, args.spot,
                     args.pred_var, rank, world, dev,
                     kernel_dtype=torch.float64 if args.dtype == "f64" else torch.float32)

@@ -1,0 +1,102 @@
+#!/bin/bash
+# The one GPU-box runner (replaces the per-session tools/gpu_r*.sh scripts).
+#
+#   STEPS="pytest,smoke,bench" O=gpurun_out/r4a bash tools/gpu.sh
+#
+# Every step runs under its own `timeout -k 10`, writes its log under $O, and a failure
+# (non-zero status, a signal, a time limit) ends the script: no GPU step runs after a
+# crashed or hung one.  Steps (in the order given):
+#   pytest        the whole GPU suite                     PYTEST_K="-k expr" narrows it
+#   pytest:FILE   one test file (tests/FILE)
+#   smoke         __graft_entry__.smoke()
+#   bench         python bench.py $BENCH_ARGS             (the driver's command by default)
+#   gloo4         CGP_BENCH_BACKEND=gloo bench.py --gpus 4 (the launcher, 4 ranks, 1 GPU)
+#   failleg       bench.py with CGP_BENCH_FAIL_LEG=mnist_as_tf (the line must still print)
+#   tile4096      bench.py --tile 4096 --steps 2 (no OOM in the stencil probe)
+#   trace:CFG     rocprofv3 --kernel-trace --stats over bench.py --config CFG
+#   pmc           PMC passes (tools/pmc.sh; PMC_CFGS) summarised into $O/net_pmc.json
+#   fullscale     tools/fullscale.py $FS_ARGS
+#   py:SCRIPT     python SCRIPT (a probe under tools/)
+#   ab            netbench (NB_ARGS) for each build in $AB: "cur" = lib/libcnngp.so, any other
+#                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=${O:-gpurun_out/run}
+mkdir -p "$O"
+
+step() {   # name limit cmd...
+    local name=$1 t=$2; shift 2
+    local t0=$SECONDS
+    timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc ($((SECONDS - t0)) s)"
+    if [ $rc -ne 0 ]; then tail -n 40 "$O/$name.log"; exit $rc; fi
+}
+
+line() {   # the bench JSON line of a log, summarised
+    python3 tools/bench_summary.py "$1"
+}
+
+IFS=',' read -ra LIST <<< "${STEPS:-pytest,smoke,bench}"
+for s in "${LIST[@]}"; do
+    case $s in
+    pytest)
+        step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+            --timeout-method thread ${PYTEST_K:-}
+        tail -n 1 "$O/pytest.log" ;;
+    pytest:*)
+        f=${s#pytest:}
+        step "pytest_${f%.py}" 900 python -u -m pytest "tests/$f" -x -v -s --timeout 600 \
+            --timeout-method thread ${PYTEST_K:-}
+        grep -E "passed|failed|worst|bit-equal" "$O/pytest_${f%.py}.log" | tail -n 12 ;;
+    smoke)
+        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+        tail -n 1 "$O/smoke.log" ;;
+    bench)
+        step bench 1200 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5}
+        line "$O/bench.log" ;;
+    gloo4)
+        CGP_BENCH_BACKEND=gloo step gloo4 900 python bench.py --gpus 4 --steps 2 --warmup 1 \
+            --no-cpu --no-f32 --no-fullscale-f32 --fullscale-n 16384 --cifar10-n 16384 \
+            --fullscale-m 4096
+        line "$O/gloo4.log" ;;
+    failleg)
+        CGP_BENCH_FAIL_LEG=mnist_as_tf step failleg 600 python bench.py --steps 2 \
+            --warmup 1 --no-cpu --no-f32 --no-fullscale --no-fullscale-cifar10 --no-cifar10
+        line "$O/failleg.log" ;;
+    tile4096)
+        step tile4096 900 python bench.py --tile 4096 --steps 2 --warmup 1 --no-cpu \
+            --no-f32 --no-fullscale --no-fullscale-cifar10 --no-second --no-cifar10
+        line "$O/tile4096.log" ;;
+    trace:*)
+        cfg=${s#trace:}
+        step "trace_$cfg" 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/trace_$cfg" \
+            -o trace -- python bench.py --config "$cfg" --steps 3 --no-cpu --no-fullscale \
+            --no-fullscale-cifar10 --no-second --no-cifar10 --no-f32
+        line "$O/trace_$cfg.log" ;;
+    pmc)
+        OUT=$O/pmc bash tools/pmc.sh > "$O/pmc.log" 2>&1 || { tail -n 30 "$O/pmc.log"; exit 1; }
+        python3 tools/pmc_r2.py "$O/pmc" "$O/net_pmc.json" > /dev/null || exit 1
+        echo "== pmc -> $O/net_pmc.json" ;;
+    fullscale)
+        step fullscale 900 python tools/fullscale.py ${FS_ARGS:-}
+        tail -n 1 "$O/fullscale.log" ;;
+    ab)
+        for rep in $(seq 1 "${AB_REPS:-2}"); do
+            for v in ${AB:-cur}; do
+                if [ "$v" = cur ]; then lib=$PWD/cnn-gp_amd/lib/libcnngp.so
+                else lib=$PWD/cnn-gp_amd/lib/ab/lib_$v.so; fi
+                CNNGP_LIB=$lib step "ab_${v}_$rep" 300 python tools/netbench.py ${NB_ARGS:-}
+                echo "-- $v (round $rep)"; grep -v amdgpu.ids "$O/ab_${v}_$rep.log" | tail -n 8
+            done
+        done ;;
+    py:*)
+        p=${s#py:}
+        step "py_$(basename "$p" .py)" 600 python "$p" ${PY_ARGS:-}
+        tail -n 30 "$O/py_$(basename "$p" .py).log" ;;
+    *)
+        echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "== done"
