@@ -341,22 +341,32 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         const double sq4 = m * __builtin_fma(-m, h, 3.0);
         sx[r] = (st[r] * u[r]) * sq4;
     }
-    if constexpr (AD != 0) {
-        // the largest x4 = 4x of the lane's pixels; the group takes the shortest polynomial
-        // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
+    if constexpr (AD == 2) {
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
         const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
-        auto all = [&](bool pred) {
-            if constexpr (AD == 1) return __all(pred) != 0;
-            else return (__ballot(pred) & seg) == ex;
-        };
-        if (all(um <= 4.0 * kReluAdaptX0)) {
+        auto all_seg = [&](bool pred) { return (__ballot(pred) & seg) == ex; };
+        if (all_seg(um <= 4.0 * kReluAdaptX0)) {
             horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
-        } else if (all(um <= 4.0 * kReluAdaptX1)) {
+        } else if (all_seg(um <= 4.0 * kReluAdaptX1)) {
             horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
-        } else if (all(um <= 4.0 * kReluAdaptX2)) {
+        } else if (all_seg(um <= 4.0 * kReluAdaptX2)) {
+            horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
+        } else {
+            horner_q<R, kReluPolyDegD>(p, u, tab.dq);
+        }
+    } else if constexpr (AD == 1) {
+        // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
+        // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
+        double um = u[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
+        if (__all(um <= 4.0 * kReluAdaptX0)) {
+            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+        } else if (__all(um <= 4.0 * kReluAdaptX1)) {
+            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        } else if (__all(um <= 4.0 * kReluAdaptX2)) {
             horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
         } else {
             horner_q<R, kReluPolyDegD>(p, u, tab.dq);

@@ -197,7 +197,9 @@ __device__ __forceinline__ int udiv(int a, int d) { return (int)((unsigned)a / (
 // the op table through a generic pointer: per-lane vector loads (the constant address
 // space's scalar loads measured -7% on ConvNet: SMEM returns count in lgkmcnt, so every
 // LDS wait also drains them)
-__device__ __forceinline__ cgp_net_op load_op(const cgp_net_op* r) {
+typedef const cgp_net_op* OpsC;
+__device__ __forceinline__ OpsC ops_c(const cgp_net_op* p) { return (OpsC)p; }
+__device__ __forceinline__ cgp_net_op load_op(OpsC r) {
     cgp_net_op o;
     o.kind = r->kind;
     o.code = r->code;
@@ -687,8 +689,8 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NHT % G::NT == 0 || it < NHT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NH), l = it - q * G::NH;
                 const int qi = udiv(l, G::NG2), g2 = l - qi * G::NG2;
-                const T* row = lds + op.src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
-                               g2 * G::R2 * G::S + G::OFF;
+                const T* row = lds + (op.src + q * arena + (G::Q0 + qi + G::OFF) * wsi +
+                                      g2 * G::R2 * G::S + G::OFF);
                 T win[G::WIN2];
 #pragma unroll
                 for (int t = 0; t < G::WIN2; ++t) win[t] = row[t];
@@ -722,7 +724,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
             if (NVT % G::NT == 0 || it < NVT) {
                 const int q = NP == 1 ? 0 : udiv(it, G::NV), l = it - q * G::NV;
                 const int g3 = udiv(l, G::WO), c = l - g3 * G::WO;
-                const T* col = lds + p.hs + q * arena + g3 * G::R3 * G::S * G::WO + c;
+                const T* col = lds + (p.hs + q * arena + g3 * G::R3 * G::S * G::WO + c);
                 T win[G::WIN3];
 #pragma unroll
                 for (int t = 0; t < G::WIN3; ++t) win[t] = col[t * G::WO];
@@ -1048,7 +1050,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
     constexpr ProgInfo I = kProgs[PID];
     if constexpr (K < I.nops) {
         constexpr ProgOp o = kProgOps[I.first + K];
-        const auto& rt = p.ops[K];
+        const auto& rt = ops_c(p.ops)[K];
         cgp_net_op op;
         op.kind = o.kind;
         op.code = o.code;
@@ -1203,7 +1205,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             const int ht = tid & (kNT - 1);
             if constexpr (PID < 0) {
                 for (int k = 0; k < p.nops; ++k) {
-                    const cgp_net_op op = load_op(p.ops + k);
+                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
                     net_op<T, EX, DU, 1>(lh, op, p, ph, ht);
                     lds_barrier();
                 }
@@ -1243,7 +1245,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             }
             if constexpr (PID < 0) {
                 for (int k = 0; k < p.nops; ++k) {
-                    const cgp_net_op op = load_op(p.ops + k);
+                    const cgp_net_op op = load_op(ops_c(p.ops) + k);
                     net_op<T, EX, DU, NP>(lds, op, p, pr, tid);
                     lds_barrier();
                 }

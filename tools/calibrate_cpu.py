@@ -8,8 +8,9 @@ the CPU.  Both are timed on the same cores with the same torch thread count, fp6
 (``.double()``, the build's dtype) and fp32 (the reference's production dtype); the
 ratio restatement/reference is what bench.py's cpu_baseline quotes next to its own
 measurement on the GPU box's host.  Also mnist_as_tf (C3's architecture) on 64 images.
-The reference is imported with the two shims SURVEY.md §8(c) records (stub torchvision,
-np.int = int); nothing of it is copied.  Output: profiles/r2/cpu_calibration.json.
+Also cifar10 (configs[4]'s network, 3×32×32) on 48 images.  The reference is imported
+with the two shims SURVEY.md §8(c) records (stub torchvision, np.int = int); nothing of
+it is copied.  Output: profiles/r4/cpu_calibration.json.
 """
 import argparse
 import importlib
@@ -59,12 +60,13 @@ def main():
            "cpu_model": next((ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo")
                               if ln.startswith("model name")), "?"),
            "torch": torch.__version__, "cases": []}
-    for cfg_name, n in (("mnist_paper_convnet_gp", 128), ("mnist_as_tf", 64)):
+    for cfg_name, n in (("mnist_paper_convnet_gp", 128), ("mnist_as_tf", 64), ("cifar10", 48)):
         cfg = imp.import_module(f"configs.{cfg_name}")
         spec = specs.CONFIGS[cfg_name]()
         g = torch.Generator().manual_seed(0)
         for dtn, dt in (("f64", torch.float64), ("f32", torch.float32)):
-            X = torch.rand((n, 1, 28, 28), generator=g, dtype=dt)
+            C, side = specs.GEOMETRY[cfg_name]
+            X = torch.rand((n, C, side, side), generator=g, dtype=dt)
             model = cfg.initial_model.to(dt)
             with torch.no_grad():
                 t_ref, k_ref = best_of(lambda: model(X), args.reps)
@@ -80,7 +82,7 @@ def main():
                 "max_rel_diff": rel})
             print(json.dumps(res["cases"][-1]), flush=True)
             cfg.initial_model.to(torch.float32)
-    out = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
+    out = os.path.join(ROOT, "profiles", "r4", "cpu_calibration.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump(res, open(out, "w"), indent=1)
     print("wrote", out)
