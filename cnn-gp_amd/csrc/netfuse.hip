@@ -1044,13 +1044,33 @@ struct ProgInfo {
 #include "net_programs.h"
 constexpr int kNumProgs = sizeof(kProgs) / sizeof(kProgs[0]);
 
+// The runtime fields of a compiled program's op records (weight, bias, variance / state
+// pointers), copied into LDS once per workgroup: an op then starts with an LDS read of its
+// pointers instead of a dependent global load of its record
+struct ProgRec {
+    double weight, bias;
+    const void* var_x;
+    const void* var_y;
+    const void* var2_x;
+    const void* var2_y;
+};
+#ifndef CGP_NET_REC_LDS
+#define CGP_NET_REC_LDS 0
+#endif
+template <int PID>
+constexpr int kRecsOf = (CGP_NET_REC_LDS && PID >= 0) ? kProgs[PID < 0 ? 0 : PID].nops : 1;
+
 template <typename T, bool DU, int NP, int PID, int K>
 __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, const Pairs& pr,
-                                         int tid) {
+                                         int tid, const ProgRec* recs) {
     constexpr ProgInfo I = kProgs[PID];
     if constexpr (K < I.nops) {
         constexpr ProgOp o = kProgOps[I.first + K];
+#if CGP_NET_REC_LDS
+        const ProgRec& rt = recs[K];
+#else
         const auto& rt = ops_c(p.ops)[K];
+#endif
         cgp_net_op op;
         op.kind = o.kind;
         op.code = o.code;
@@ -1094,7 +1114,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
             net_move<T, o.kind, NP>(lds, op, p, pr);
         }
         lds_barrier();
-        prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid);
+        prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid, recs);
     }
 }
 
@@ -1135,6 +1155,13 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     const int tid = threadIdx.x;
     constexpr int UN = kUnitsOf<NP>;
     for (int e = tid; e < UN * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
+    __shared__ ProgRec prog_recs[kRecsOf<PID>];
+    if constexpr (PID >= 0 && CGP_NET_REC_LDS) {
+        for (int k = tid; k < kRecsOf<PID>; k += kNTof<NP>) {
+            const cgp_net_op& r = p.ops[k];
+            prog_recs[k] = ProgRec{r.weight, r.bias, r.var_x, r.var_y, r.var2_x, r.var2_y};
+        }
+    }
     lds_barrier();
     // XCD-contiguous work ranges: workgroup b runs on XCD b % 8, so each XCD walks one
     // contiguous run of supertiles and its L2 holds the images/variances they share.
@@ -1210,7 +1237,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
                     lds_barrier();
                 }
             } else {
-                prog_ops<T, DU, 1, PID, 0>(lh, p, ph, ht);
+                prog_ops<T, DU, 1, PID, 0>(lh, p, ph, ht, prog_recs);
             }
             if (p.final_stage && ht == 0 && vq) {
                 if (wq) {
@@ -1250,7 +1277,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
                     lds_barrier();
                 }
             } else {
-                prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid);
+                prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid, prog_recs);
             }
             if (p.final_stage) {
                 if constexpr (NP == 1) {
@@ -1437,9 +1464,20 @@ unsigned long long* work_counters(hipStream_t s) {
 template <typename T>
 int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, int program,
                void* stream) {
-    const long long wg_bytes = lds_bytes * net_units(np);
+    long long wg_bytes = lds_bytes * net_units(np);
     const void* fn = program > 0 && !ex ? prog_fn<T>(program - 1) : net_fn<T>(ex, du, np, wg_bytes);
     if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
+    // occupancy probe (diagnostic, round 4): CGP_NET_MAX_WG=N reserves enough LDS that at
+    // most N two-pair head workgroups fit a CU
+    if (np == 2) {
+        if (const char* cap = getenv("CGP_NET_MAX_WG")) {
+            const long long n = atoll(cap);
+            if (n > 0 && wg_bytes <= 163840 / n) {
+                const long long pad = 163840 / (n + 1) + 256;
+                if (pad > wg_bytes && pad <= 163840 / n) wg_bytes = pad;
+            }
+        }
+    }
     const int per_cu = net_occupancy(fn, (int)wg_bytes, net_threads(np));
     if (per_cu <= 0)
         return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", wg_bytes);

@@ -183,9 +183,10 @@ def test_save_K_with_device_kern_matches_reference_files(n_workers):
     assert f.d["Kx_diag"].chunks == tuple(z["Kx_diag_chunks"])
 
 
-def _pipeline_rank(rank, world, port, q):
+def _pipeline_rank(rank, world, port, q, backend="gloo"):
     """cnn_gp.pipeline.classify_distributed with the HIP model, rocSOLVER and the device
-    score product: world 1 in-process (rank None) or one gloo rank of a world"""
+    score product: world 1 in-process (rank None) or one rank of a world — gloo ranks
+    share GPU 0, nccl (RCCL) ranks run one per GPU"""
     import sys
     from conftest import PKG, ROOT
     sys.path[:0] = [PKG, ROOT]
@@ -196,9 +197,14 @@ def _pipeline_rank(rank, world, port, q):
     if world > 1:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if backend == "nccl" else 0
+    torch.cuda.set_device(dev)
+    if world > 1:
+        from datetime import timedelta
+        kw = {"device_id": torch.device("cuda", dev)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=timedelta(seconds=120), **kw)
     try:
-        torch.cuda.set_device(0)
         m = configs_util.model("mnist_as_tf").to("cuda", torch.float64)
         X = _images(200, 5).cuda()
         Z = _images(70, 6).cuda()
@@ -229,16 +235,14 @@ def _pipeline_rank(rank, world, port, q):
         q.put(out)
 
 
-def test_world2_pipeline_on_device_matches_single_process():
-    """Row strips of Kxx gathered point-to-point, solve on rank 0 while rank 1 builds its
-    Kxz rows, α broadcast, scores gathered: α and the predicted labels bit-equal to the
-    one-process run, Kxz (gathered on request) bit-equal too"""
+def _world2_pipeline(backend):
     single = _pipeline_rank(None, 1, None, None)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipeline_rank, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipeline_rank, args=(r, world, port, q, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -255,5 +259,20 @@ def test_world2_pipeline_on_device_matches_single_process():
     assert np.array_equal(res["pred"], single["pred"])
     assert np.array_equal(res["Kxz"], single["Kxz"])
     np.testing.assert_allclose(res["scores"], single["scores"], rtol=1e-12, atol=1e-12)
-    print(f"rank-0 device peak in the gather + solve: {res['peak_gather_solve'] / 1e6:.1f} MB "
-          f"(Kxx {200 * 200 * 8 / 1e6:.2f} MB)")
+    print(f"{backend}: rank-0 device peak in the gather + solve: "
+          f"{res['peak_gather_solve'] / 1e6:.1f} MB (Kxx {200 * 200 * 8 / 1e6:.2f} MB)")
+
+
+def test_world2_pipeline_on_device_matches_single_process():
+    """Row strips of Kxx gathered point-to-point, solve on rank 0 while rank 1 builds its
+    Kxz rows, α broadcast, scores gathered: α and the predicted labels bit-equal to the
+    one-process run, Kxz (gathered on request) bit-equal too (two gloo ranks sharing the
+    GPU)"""
+    _world2_pipeline("gloo")
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL ranks need two GPUs")
+def test_world2_nccl_pipeline_matches_single_process():
+    """The same over RCCL, one rank per GPU: batch_isend_irecv of the Kxx strips, the
+    device all_reduce of the phase times, the broadcast of the solve status and of α"""
+    _world2_pipeline("nccl")

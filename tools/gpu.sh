@@ -16,9 +16,11 @@
 #   trace:CFG     rocprofv3 --kernel-trace --stats over bench.py --config CFG
 #   pmc           PMC passes (tools/pmc.sh; PMC_CFGS) summarised into $O/net_pmc.json
 #   fullscale     tools/fullscale.py $FS_ARGS
+#   occ           netbench (NB_ARGS) with CGP_NET_MAX_WG = each of OCC_CAPS (0 = uncapped)
 #   py:SCRIPT     python SCRIPT (a probe under tools/)
 #   ab            netbench (NB_ARGS) for each build in $AB: "cur" = lib/libcnngp.so, any other
-#                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds
+#                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds;
+#                 AB_TEST=1 runs each variant's whole-network parity tests first
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -83,6 +85,15 @@ for s in "${LIST[@]}"; do
         step fullscale 900 python tools/fullscale.py ${FS_ARGS:-}
         tail -n 1 "$O/fullscale.log" ;;
     ab)
+        if [ -n "${AB_TEST:-}" ]; then   # each variant's whole-network parity first
+            for v in ${AB:-cur}; do
+                [ "$v" = cur ] && continue
+                CNNGP_LIB=$PWD/cnn-gp_amd/lib/ab/lib_$v.so step "abtest_$v" 600 python -u -m \
+                    pytest tests/test_gpu_parity.py -x -q -k "netfuse or e2e or program" \
+                    --timeout 300 --timeout-method thread
+                tail -n 1 "$O/abtest_$v.log"
+            done
+        fi
         for rep in $(seq 1 "${AB_REPS:-2}"); do
             for v in ${AB:-cur}; do
                 if [ "$v" = cur ]; then lib=$PWD/cnn-gp_amd/lib/libcnngp.so
@@ -91,6 +102,17 @@ for s in "${LIST[@]}"; do
                 echo "-- $v (round $rep)"; grep -v amdgpu.ids "$O/ab_${v}_$rep.log" | tail -n 8
             done
         done ;;
+    occ)
+        # head-stage occupancy probe: CGP_NET_MAX_WG caps the two-pair workgroups per CU
+        for rep in 1 2; do
+            for cap in ${OCC_CAPS:-0 5 4 3}; do
+                if [ "$cap" = 0 ]; then unset CGP_NET_MAX_WG; else export CGP_NET_MAX_WG=$cap; fi
+                step "occ_${cap}_$rep" 300 python tools/netbench.py ${NB_ARGS:-}
+                echo "-- max workgroups per CU: $cap (round $rep)"
+                grep -v amdgpu.ids "$O/occ_${cap}_$rep.log" | tail -n 8
+            done
+        done
+        unset CGP_NET_MAX_WG ;;
     py:*)
         p=${s#py:}
         step "py_$(basename "$p" .py)" 600 python "$p" ${PY_ARGS:-}
