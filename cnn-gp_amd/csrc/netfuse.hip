@@ -1046,7 +1046,10 @@ constexpr int kNumProgs = sizeof(kProgs) / sizeof(kProgs[0]);
 
 // The runtime fields of a compiled program's op records (weight, bias, variance / state
 // pointers), copied into LDS once per workgroup: an op then starts with an LDS read of its
-// pointers instead of a dependent global load of its record
+// pointers instead of a dependent global load of its record (round 4, one B = 1024 Kxz tile,
+// two rounds in one call, profiles/r4/ab_r4d_rec_pre.log: ConvNet +1.2%, mnist_as_tf +1.8%,
+// cifar10 +2.7%).  Issuing op k + 1's variance loads at the end of op k instead measured
+// -2.8% on ConvNet and neutral elsewhere (same log): the wave priority already overlaps them.
 struct ProgRec {
     double weight, bias;
     const void* var_x;
@@ -1054,44 +1057,52 @@ struct ProgRec {
     const void* var2_x;
     const void* var2_y;
 };
-#ifndef CGP_NET_REC_LDS
-#define CGP_NET_REC_LDS 0
-#endif
 template <int PID>
-constexpr int kRecsOf = (CGP_NET_REC_LDS && PID >= 0) ? kProgs[PID < 0 ? 0 : PID].nops : 1;
+constexpr int kRecsOf = PID >= 0 ? kProgs[PID < 0 ? 0 : PID].nops : 1;
 
+// op K of program PID as a record: compile-time fields from the program, runtime ones
+// (weight, bias, variance / state pointers) from the launch's op records
+template <int PID, int K>
+__device__ __forceinline__ cgp_net_op prog_op(const ProgRec* recs) {
+    constexpr ProgOp o = kProgOps[kProgs[PID].first + K];
+    const ProgRec& rt = recs[K];
+    cgp_net_op op;
+    op.kind = o.kind;
+    op.code = o.code;
+    op.src = o.src;
+    op.dst = o.dst;
+    op.add = o.add;
+    op.ws_in = o.ws_in;
+    op.ws_out = o.ws_out;
+    op.relu = o.relu;
+    op.h = o.h;
+    op.w = o.w;
+    op.div_m = 0;
+    op.div_s = 0;
+    op.dst2 = o.dst2;
+    op.zero_halo = o.zero_halo;
+    op.weight = rt.weight;
+    op.bias = rt.bias;
+    op.var_x = rt.var_x;
+    op.var_y = rt.var_y;
+    op.var2_x = rt.var2_x;
+    op.var2_y = rt.var2_y;
+    return op;
+}
+// the conv geometry of a program op
+template <int PID, int K, int NP>
+struct ProgGeo {
+    static constexpr ProgOp o = kProgOps[kProgs[PID].first + K];
+    static constexpr GeoRow g = kGeoTable[o.code & (CGP_NET_CODE_HS_CLEAN - 1)];
+    using G = NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>;
+};
 template <typename T, bool DU, int NP, int PID, int K>
 __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, const Pairs& pr,
                                          int tid, const ProgRec* recs) {
     constexpr ProgInfo I = kProgs[PID];
     if constexpr (K < I.nops) {
         constexpr ProgOp o = kProgOps[I.first + K];
-#if CGP_NET_REC_LDS
-        const ProgRec& rt = recs[K];
-#else
-        const auto& rt = ops_c(p.ops)[K];
-#endif
-        cgp_net_op op;
-        op.kind = o.kind;
-        op.code = o.code;
-        op.src = o.src;
-        op.dst = o.dst;
-        op.add = o.add;
-        op.ws_in = o.ws_in;
-        op.ws_out = o.ws_out;
-        op.relu = o.relu;
-        op.h = o.h;
-        op.w = o.w;
-        op.div_m = 0;
-        op.div_s = 0;
-        op.dst2 = o.dst2;
-        op.zero_halo = o.zero_halo;
-        op.weight = rt.weight;
-        op.bias = rt.bias;
-        op.var_x = rt.var_x;
-        op.var_y = rt.var_y;
-        op.var2_x = rt.var2_x;
-        op.var2_y = rt.var2_y;
+        const cgp_net_op op = prog_op<PID, K>(recs);
         if constexpr (o.zero_halo != 0) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
@@ -1104,9 +1115,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
             }
         }
         if constexpr (o.kind == CGP_NET_CONV) {
-            constexpr GeoRow g = kGeoTable[o.code & (CGP_NET_CODE_HS_CLEAN - 1)];
-            net_conv<T, false, DU, NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>>(lds, op, p,
-                                                                                    pr);
+            net_conv<T, false, DU, typename ProgGeo<PID, K, NP>::G>(lds, op, p, pr);
         } else if constexpr (o.kind == CGP_NET_RELU || o.kind == CGP_NET_LINEAR ||
                              o.kind == CGP_NET_MOMENTS) {
             net_elem<T, false, DU, o.kind, o.h, o.w, NP>(lds, op, p, pr);
@@ -1156,7 +1165,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     constexpr int UN = kUnitsOf<NP>;
     for (int e = tid; e < UN * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
     __shared__ ProgRec prog_recs[kRecsOf<PID>];
-    if constexpr (PID >= 0 && CGP_NET_REC_LDS) {
+    if constexpr (PID >= 0) {
         for (int k = tid; k < kRecsOf<PID>; k += kNTof<NP>) {
             const cgp_net_op& r = p.ops[k];
             prog_recs[k] = ProgRec{r.weight, r.bias, r.var_x, r.var_y, r.var2_x, r.var2_y};
