@@ -20,7 +20,9 @@
 #   py:SCRIPT     python SCRIPT (a probe under tools/)
 #   ab            netbench (NB_ARGS) for each build in $AB: "cur" = lib/libcnngp.so, any other
 #                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds;
-#                 AB_TEST=1 runs each variant's whole-network parity tests first
+#                 AB_TEST=1 runs each variant's whole-network parity tests first; a NAME=VALUE
+#                 entry runs the current library with that environment variable
+#   envtest       pytest $PYTEST_ARGS with the environment ENVTEST="NAME=VALUE ..."
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -96,12 +98,24 @@ for s in "${LIST[@]}"; do
         fi
         for rep in $(seq 1 "${AB_REPS:-2}"); do
             for v in ${AB:-cur}; do
-                if [ "$v" = cur ]; then lib=$PWD/cnn-gp_amd/lib/libcnngp.so
-                else lib=$PWD/cnn-gp_amd/lib/ab/lib_$v.so; fi
-                CNNGP_LIB=$lib step "ab_${v}_$rep" 300 python tools/netbench.py ${NB_ARGS:-}
-                echo "-- $v (round $rep)"; grep -v amdgpu.ids "$O/ab_${v}_$rep.log" | tail -n 8
+                # NAME=VALUE: the current library with that environment variable set
+                lib=$PWD/cnn-gp_amd/lib/libcnngp.so; envset=""; tag=$v
+                case $v in
+                cur) ;;
+                *=*) envset=$v; tag=${v//[^A-Za-z0-9]/_} ;;
+                *) lib=$PWD/cnn-gp_amd/lib/ab/lib_$v.so ;;
+                esac
+                env $envset CNNGP_LIB=$lib bash -c "$(declare -f step); O=$O; \
+                    step ab_${tag}_$rep 300 python tools/netbench.py ${NB_ARGS:-}" || exit 1
+                echo "-- $v (round $rep)"; grep -v amdgpu.ids "$O/ab_${tag}_$rep.log" | tail -n 8
             done
         done ;;
+    envtest)
+        # parity under an environment setting: ENVTEST="NAME=VALUE" PYTEST_ARGS="files -k expr"
+        env ${ENVTEST} bash -c "$(declare -f step); O=$O; step envtest 900 python -u -m \
+            pytest ${PYTEST_ARGS:-tests/test_gpu_parity.py} -x -q --timeout 300 \
+            --timeout-method thread" || exit 1
+        tail -n 1 "$O/envtest.log" ;;
     occ)
         # head-stage occupancy probe: CGP_NET_MAX_WG caps the two-pair workgroups per CU
         for rep in 1 2; do
