@@ -420,9 +420,7 @@ def net_roofline(model, x, cfg_name, timing):
             "frac_incl_pointwise": round(achieved_pw / FP64_PEAK_TFLOPS, 4),
             "valu_insts_per_pair": valu_insts,
             "ops_per_pair": net.n_ops, "lds_bytes": net.lds_elems * x.element_size(),
-            "stages": [{"pairs_per_workgroup": N.load().cgp_net_units(st.pairs),
-                        "threads": {2: 256, N.CGP_NET_PAIRS_WIDE4: 448}.get(st.pairs, 128),
-                        "ops": st.n_ops} for st in net.stages],
+            "stages": [{"pairs_per_workgroup": st.pairs, "ops": st.n_ops} for st in net.stages],
             "note": "bound valu_f64: the kernel keeps every map in LDS (HBM carries images, "
                     "L2-resident variance maps and one entry per pair); peak = fp64 VALU "
                     "(= fp64 MFMA) 78.6 TF; achieved = credited direct-stencil conv flops of "

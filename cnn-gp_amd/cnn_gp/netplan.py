@@ -109,19 +109,13 @@ MULTI_PAIR = ((16, 64), (4, 256))
 # in one four-wave workgroup (csrc/netfuse.hip net_kernel, NP == 2: units u and u + 1, the
 # same image i), 1 one pair on two waves.  Measured on the MI355X (one B = 1024 Kxz tile):
 # ConvNet GP +13%, mnist_as_tf / cifar10 +1%, Residual CNN GP even.  CGP_NET_PAIRS0=1
-# selects one pair per workgroup; CGP_NET_PAIRS0=w4 four pairs on seven waves
-# (N.CGP_NET_PAIRS_WIDE4) where a compiled program for it exists.
+# selects one pair per workgroup.
 FIRST_PAIRS = os.environ.get("CGP_NET_PAIRS0", "2")
-# a wide first stage is kept only when the library has its compiled program (off only while
-# tools/gen_net_programs.py enumerates the candidates)
-WIDE_NEEDS_PROGRAM = True
 
 
 def first_pairs(n_stages: int) -> int:
-    """Pairs code of the first of n_stages stages."""
+    """Pairs per workgroup of the first of n_stages stages."""
     del n_stages
-    if FIRST_PAIRS == "w4":
-        return N.CGP_NET_PAIRS_WIDE4
     return 2 if FIRST_PAIRS in ("2", "auto") else 1
 MIN_STAGE_OPS = 4                      # a shorter tail is not worth a launch + state
 # state buffers: units per launch group (each group runs every stage once, and each launch
@@ -205,12 +199,7 @@ class NetPlan:
             ins = sorted(v for v, pi in prod.items() if pi < lo and last.get(v, -1) >= lo)
             outs = sorted(v for v, pi in prod.items() if pi < hi <= last.get(v, -1)) \
                 if hi < len(lowered) else []
-            if np_ == N.CGP_NET_PAIRS_WIDE4:
-                st = self._wide_stage(lowered, lo, hi, ins, outs, last, dual, itemsize)
-                if st is None:
-                    np_ = 2
-            if np_ != N.CGP_NET_PAIRS_WIDE4:
-                st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
+            st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
             # the two-pair workgroup holds cgp_net_units(2) one-pair arenas
             if np_ == 2 and st.lds_elems * itemsize * lib.cgp_net_units(2) > MAX_LDS_BYTES:
                 st = self._lower(lowered, lo, hi, 1, ins, outs, last, dual, itemsize)
@@ -227,7 +216,7 @@ class NetPlan:
 
     @property
     def lds_elems(self):
-        return max(st.lds_elems * self._lib.cgp_net_units(st.pairs) for st in self.stages)
+        return max(st.lds_elems * st.pairs for st in self.stages)
 
     @property
     def final_slot(self):
@@ -296,41 +285,9 @@ class NetPlan:
         # the first stage on 2 pairs: two one-pair halves of one workgroup (any op list;
         # __init__ falls back to 1 when twice the arena does not fit the LDS)
         lo0, hi0, _ = bounds[0]
-        fp = first_pairs(len(bounds))
-        if fp != 1:
-            bounds[0] = (lo0, hi0, fp)
+        if first_pairs(len(bounds)) == 2:
+            bounds[0] = (lo0, hi0, 2)
         return bounds
-
-    def _wide_stage(self, lowered, lo, hi, ins, outs, last, dual, itemsize):
-        """The stage lowered[lo:hi] as four pairs on seven waves (N.CGP_NET_PAIRS_WIDE4),
-        or None: it must hold no full-map reduction (its per-pair lanes would straddle
-        waves), no map above 28x28, fit the LDS four times, and match a compiled program
-        (the library has no interpreter for it)."""
-        if not USE_PROGRAMS:
-            return None
-        shapes = self._shapes
-        for idx in range(lo, hi):
-            kind, a, op = lowered[idx]
-            if kind != "op":
-                continue
-            for v in [op.dst] + self._sources(op):
-                if shapes[v][0] * shapes[v][1] > 28 * 28:
-                    return None
-            if op.kind == "conv" and tuple(op.shape_out) == (1, 1):
-                return None
-        st = self._lower(lowered, lo, hi, 4, ins, outs, last, dual, itemsize)
-        if st.lds_elems * itemsize * 4 > MAX_LDS_BYTES:
-            return None
-        st.pairs = N.CGP_NET_PAIRS_WIDE4
-        dummy = torch.zeros(8, dtype=torch.float64)
-        var = {v: (dummy, dummy) for _, v in st.records if v is not None}
-        var.update({f["var2"]: (dummy, dummy) for f, _ in st.records if "var2" in f})
-        arr = self._ops_array(st, var, dummy, dummy)
-        flags = N.CGP_FLAG_NET_DUAL if st.dual else 0
-        if WIDE_NEEDS_PROGRAM and not self._lib.cgp_net_program(
-                ctypes.byref(arr), st.n_ops, st.pairs, flags, st.lds_elems, itemsize):
-            return None
-        return st
 
     def _lower(self, lowered, lo, hi, pairs, ins, outs, last, dual, itemsize):
         """Slots and records of lowered[lo:hi] (inputs loaded from the incoming state

@@ -39,18 +39,11 @@ constexpr int kNT = 128;  // threads per workgroup (one pair): two waves
 // pairs on two waves.  Ops only ever run on one half (NP = 1) or on NP = 4 / 16.  (Four
 // one-pair slices on 512 threads measured -15% fp64: LDS then admits 2 workgroups per CU.)
 constexpr int kSplit = 2;
-// CGP_NET_PAIRS_WIDE4 (cnngp.h): four pairs on seven waves, so a 28x28 pass's 4 x 112
-// items fill all 448 lanes (compiled programs only).  Template code: NPC = the pairs
-// code, NP = its pair count.
-constexpr int kWide4 = CGP_NET_PAIRS_WIDE4;
-constexpr int kWideNT = 448;
-template <int NPC>
-constexpr int kPairsOf = NPC == kWide4 ? 4 : NPC;
-template <int NPC>
-constexpr int kNTof = NPC == 2 ? kSplit * kNT : NPC == kWide4 ? kWideNT : kNT;
+template <int NP>
+constexpr int kNTof = NP == 2 ? kSplit * kNT : kNT;
 // pair units a workgroup takes per step of the walk
-template <int NPC>
-constexpr int kUnitsOf = NPC == 2 ? kSplit : kPairsOf<NPC>;
+template <int NP>
+constexpr int kUnitsOf = NP == 2 ? kSplit : NP;
 constexpr int kSTL = 3;             // log2(kST) (16² / 32² supertiles measured ±0.7%)
 constexpr int kST = 1 << kSTL;      // supertile edge: pairs are walked in 8x8 (i, j) blocks
 constexpr int kEw = 4;          // elementwise ops: pixels per thread per pass
@@ -74,12 +67,11 @@ constexpr int pick_r(int lines, int len, int taps, int s, int epi, int nt) {
 }
 
 // NP_: pairs per workgroup (their items share the passes; per-pair counts below)
-template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_, int NP_ = 1,
-          int NT_ = kNT>
+template <int H_, int W_, int HO_, int WO_, int TAPS_, int S_, int OFF_, int NP_ = 1>
 struct NG {
     static constexpr int H = H_, W = W_, HO = HO_, WO = WO_, TAPS = TAPS_, S = S_, OFF = OFF_;
     static constexpr int NP = NP_;
-    static constexpr int NT = NT_;
+    static constexpr int NT = kNT;
     static_assert(NP_ != 2, "two-pair workgroups run their ops as one-pair halves");
     static constexpr int HW = H * W, HOWO = HO * WO;
     static constexpr bool POINT = TAPS == 1 && OFF == 0;
@@ -191,15 +183,10 @@ __device__ __forceinline__ void win_sums(const T (&w)[(R - 1) * S + TAPS], T (&o
 // registers for every geometry at once (hoisted: -1% fp64, scratch spills in the head
 // programs)
 // (thread index within its 128-thread half: a two-pair workgroup runs one pair per half)
-// (a wide stage's 448 threads all work on one set of pairs: no mask)
-template <int NT = kNT>
 __device__ __forceinline__ int opaque_tid() {
     static_assert(kNT == 128, "opaque_tid masks to 128-thread halves");
     int t;
-    if constexpr (NT == kNT)
-        asm volatile("v_and_b32 %0, 0x7f, %1" : "=v"(t) : "v"((int)threadIdx.x));
-    else
-        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    asm volatile("v_and_b32 %0, 0x7f, %1" : "=v"(t) : "v"((int)threadIdx.x));
     return t;
 }
 
@@ -489,7 +476,7 @@ template <typename T, bool EX, bool DU, class G>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, const Pairs& pr) {
     constexpr int NP = G::NP;
-    const int tid = opaque_tid<G::NT>();
+    const int tid = opaque_tid();
     const PolyTab tab = poly_table();
     // a conv feeding the fp64 closed-form ReLU produces c/4 (exact: w/4, b/4) for relu_q_n
     const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
@@ -767,7 +754,7 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 // ---- elementwise ops: RELU, LINEAR, MOMENTS -------------------------------------------
 // One pass: KE pixels per thread at e = base + k·NT + tid over the NP pairs' maps
 // (pair q = e / hw; NP > 1 needs the compile-time size W_).
-template <typename T, bool EX, bool DU, int KIND, int KE, int W_, int NP, int NT = kNT>
+template <typename T, bool EX, bool DU, int KIND, int KE, int W_, int NP>
 __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op& op,
                                           const NetP<T>& p, const Pairs& pr, int tid,
                                           int base, int hw, const PolyTab& tab) {
@@ -799,7 +786,7 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
     bool ok[KE];
 #pragma unroll
     for (int k = 0; k < KE; ++k) {
-        const int e = base + k * NT + tid;
+        const int e = base + k * kNT + tid;
         ok[k] = e < n;
         const int ec = ok[k] ? e : 0;
         const int q = NP == 1 ? 0 : ec / hw, pc = ec - q * hw;
@@ -816,21 +803,11 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
         if constexpr (KIND == CGP_NET_RELU) {
             a[k] = lds[op.src + at[k]];
         } else if constexpr (KIND == CGP_NET_MOMENTS) {
-            // one pair: the images' offsets folded into the scalar bases; several (a wide
-            // stage): 32-bit per-lane byte offsets of pair q's images (net_impl bounds them)
-            unsigned xo = 0, yo = 0;
-            if constexpr (NP > 1) {
-                unsigned iq, jq;
-                pair_q<NP>(pr, q, iq, jq);
-                xo = iq * (unsigned)(p.channels * hw) * (unsigned)sizeof(T);
-                yo = jq * (unsigned)(p.channels * hw) * (unsigned)sizeof(T);
-            }
-            const GP<char> xb = NP == 1 ? xi : ubase(p.x) + xo;
-            const GP<char> yb = NP == 1 ? yj : ubase(p.y) + yo;
-            T acc = img(xb, (unsigned)pc) * img(yb, (unsigned)pc);
+            static_assert(NP == 1, "moments run one pair per workgroup (half)");
+            T acc = img(xi, (unsigned)pc) * img(yj, (unsigned)pc);
             for (int ch = 1; ch < p.channels; ++ch) {
                 const unsigned e = (unsigned)(ch * hw + pc);
-                acc += img(xb, e) * img(yb, e);
+                acc += img(xi, e) * img(yj, e);
             }
             a[k] = acc;
         } else {
@@ -868,45 +845,44 @@ __device__ __forceinline__ void elem_pass(T* __restrict__ lds, const cgp_net_op&
 
 // compile-time map size: passes of at most kEw pixels per thread, the last one sized to
 // what is left (28x28: 4 + 3)
-template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP, int PI, int NT = kNT>
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP, int PI>
 __device__ __forceinline__ void elem_passes(T* __restrict__ lds, const cgp_net_op& op,
                                             const NetP<T>& p, const Pairs& pr, int tid,
                                             const PolyTab& tab) {
-    constexpr int KF = (NP * H_ * W_ + NT - 1) / NT;
+    constexpr int KF = (NP * H_ * W_ + kNT - 1) / kNT;
     if constexpr (PI * kEw < KF) {
         constexpr int KE = KF - PI * kEw < kEw ? KF - PI * kEw : kEw;
-        elem_pass<T, EX, DU, KIND, KE, W_, NP, NT>(lds, op, p, pr, tid, PI * kEw * NT,
-                                                   H_ * W_, tab);
-        elem_passes<T, EX, DU, KIND, H_, W_, NP, PI + 1, NT>(lds, op, p, pr, tid, tab);
+        elem_pass<T, EX, DU, KIND, KE, W_, NP>(lds, op, p, pr, tid, PI * kEw * kNT, H_ * W_,
+                                               tab);
+        elem_passes<T, EX, DU, KIND, H_, W_, NP, PI + 1>(lds, op, p, pr, tid, tab);
     }
 }
 
 // H_ = W_ = 0: runtime map size (generic path, one pair per workgroup).
-template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP, int NT = kNT>
+template <typename T, bool EX, bool DU, int KIND, int H_, int W_, int NP>
 __device__ __forceinline__ void net_elem(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, const Pairs& pr) {
-    static_assert(NT == kNT || H_ > 0, "wide stages run compile-time map sizes");
-    const int tid = opaque_tid<NT>();
+    const int tid = opaque_tid();
     const PolyTab tab = poly_table();
     if constexpr (H_ == 0) {
         const int hw = op.h * op.w;
         for (int base = 0; base < hw; base += kEw * kNT)
             elem_pass<T, EX, DU, KIND, kEw, 0, 1>(lds, op, p, pr, tid, base, hw, tab);
     } else {
-        elem_passes<T, EX, DU, KIND, H_, W_, NP, 0, NT>(lds, op, p, pr, tid, tab);
+        elem_passes<T, EX, DU, KIND, H_, W_, NP, 0>(lds, op, p, pr, tid, tab);
     }
 }
 
 // Stage boundary (CGP_NET_LOAD / CGP_NET_STORE): the map of each of the NP pairs moves
 // between its slot and the unit's state record, state[(u - ubeg) · code + add + pixel].
-template <typename T, int KIND, int NP, int NT = kNT>
+template <typename T, int KIND, int NP>
 __device__ __forceinline__ void net_move(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, const Pairs& pr) {
-    const int tid = opaque_tid<NT>();
+    const int tid = opaque_tid();
     const int hw = op.h * op.w, n = NP * hw;
     const int arena = NP == 1 ? 0 : p.lds_elems;
     T* state = const_cast<T*>(static_cast<const T*>(op.var_x));
-    for (int e = tid; e < n; e += NT) {
+    for (int e = tid; e < n; e += kNT) {
         const int q = NP == 1 ? 0 : e / hw, l = e - q * hw;
         const int r = l / op.w, c = l - r * op.w;
         // the state buffer holds the units of this launch, [ubeg, uend)
@@ -1114,14 +1090,13 @@ __device__ __forceinline__ cgp_net_op prog_op(const ProgRec* recs) {
     return op;
 }
 // the conv geometry of a program op
-template <int PID, int K, int NP, int NT>
+template <int PID, int K, int NP>
 struct ProgGeo {
     static constexpr ProgOp o = kProgOps[kProgs[PID].first + K];
     static constexpr GeoRow g = kGeoTable[o.code & (CGP_NET_CODE_HS_CLEAN - 1)];
-    using G = NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP, NT>;
+    using G = NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>;
 };
-// NP pairs on NT threads (one-pair halves: NP = 1, NT = 128)
-template <typename T, bool DU, int NP, int PID, int K, int NT = kNT>
+template <typename T, bool DU, int NP, int PID, int K>
 __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, const Pairs& pr,
                                          int tid, const ProgRec* recs) {
     constexpr ProgInfo I = kProgs[PID];
@@ -1132,22 +1107,23 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 const int qa = q * I.lds_elems;
-                zero_halos<T, NT>(lds + qa, o.dst, o.zero_halo & 0xffff, o.h, o.w,
-                                  o.ws_out, tid);
-                zero_halos<T, NT>(lds + qa, o.dst2, (unsigned)o.zero_halo >> 16, o.h, o.w,
-                                  o.ws_out, tid);
+                zero_halos<T, kNT>(lds + qa, o.dst, o.zero_halo & 0xffff, o.h, o.w,
+                                         o.ws_out, tid);
+                zero_halos<T, kNT>(lds + qa, o.dst2, (unsigned)o.zero_halo >> 16, o.h, o.w,
+                                         o.ws_out,
+                           tid);
             }
         }
         if constexpr (o.kind == CGP_NET_CONV) {
-            net_conv<T, false, DU, typename ProgGeo<PID, K, NP, NT>::G>(lds, op, p, pr);
+            net_conv<T, false, DU, typename ProgGeo<PID, K, NP>::G>(lds, op, p, pr);
         } else if constexpr (o.kind == CGP_NET_RELU || o.kind == CGP_NET_LINEAR ||
                              o.kind == CGP_NET_MOMENTS) {
-            net_elem<T, false, DU, o.kind, o.h, o.w, NP, NT>(lds, op, p, pr);
+            net_elem<T, false, DU, o.kind, o.h, o.w, NP>(lds, op, p, pr);
         } else if constexpr (o.kind == CGP_NET_LOAD || o.kind == CGP_NET_STORE) {
-            net_move<T, o.kind, NP, NT>(lds, op, p, pr);
+            net_move<T, o.kind, NP>(lds, op, p, pr);
         }
         lds_barrier();
-        prog_ops<T, DU, NP, PID, K + 1, NT>(lds, p, pr, tid, recs);
+        prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid, recs);
     }
 }
 
@@ -1180,21 +1156,17 @@ int prog_match(const cgp_net_op* ops, int nops, int pairs, int dual, int lds_ele
 // LDS footprint (net_wpe).  NP: pairs per workgroup (1; 2 on four waves, sharing image i;
 // 4 / 16 for small-map stages).
 // PID >= 0: compiled program PID instead of the op-record interpreter.
-template <typename T, bool EX, bool DU, int WPE, int NPC, int PID = -1>
-__global__ __launch_bounds__(kNTof<NPC>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
-    // NPC: the pairs code (1, 2 = one-pair halves, 4, 16, kWide4); NP pairs on NTH threads
-    constexpr int NP = kPairsOf<NPC>;
-    constexpr int NTH = kNTof<NPC>;
-    static_assert(NPC != kWide4 || PID >= 0, "wide stages run compiled programs only");
+template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
+__global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     __shared__ unsigned pair_tab[2 * kMaxNP];
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
-    constexpr int UN = kUnitsOf<NPC>;
-    for (int e = tid; e < UN * p.lds_elems; e += NTH) lds[e] = T(0);   // halos stay zero
+    constexpr int UN = kUnitsOf<NP>;
+    for (int e = tid; e < UN * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
     __shared__ ProgRec prog_recs[kRecsOf<PID>];
     if constexpr (PID >= 0) {
-        for (int k = tid; k < kRecsOf<PID>; k += NTH) {
+        for (int k = tid; k < kRecsOf<PID>; k += kNTof<NP>) {
             const cgp_net_op& r = p.ops[k];
             prog_recs[k] = ProgRec{r.weight, r.bias, r.var_x, r.var_y, r.var2_x, r.var2_y};
         }
@@ -1231,7 +1203,7 @@ __global__ __launch_bounds__(kNTof<NPC>) __attribute__((amdgpu_waves_per_eu(WPE)
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
-        if constexpr (NPC == 2) {
+        if constexpr (NP == 2) {
             // one-pair slices sharing the workgroup's barriers: waves 2q, 2q + 1 run unit
             // u + q (the next j of the same image i), each on its own arena.  The pair is
             // uniform per wave, so each slice runs the one-pair code (scalar variance-map
@@ -1314,7 +1286,7 @@ __global__ __launch_bounds__(kNTof<NPC>) __attribute__((amdgpu_waves_per_eu(WPE)
                     lds_barrier();
                 }
             } else {
-                prog_ops<T, DU, NP, PID, 0, NTH>(lds, p, pr, tid, prog_recs);
+                prog_ops<T, DU, NP, PID, 0>(lds, p, pr, tid, prog_recs);
             }
             if (p.final_stage) {
                 if constexpr (NP == 1) {
@@ -1408,11 +1380,8 @@ const void* prog_fn_one() {
     } else {
         constexpr long long bytes =
             (long long)I.lds_elems * (long long)sizeof(T) * kUnitsOf<I.pairs>;
-        // a wide stage's seven-wave workgroups fit a CU twice at 4 or 5 waves per SIMD (a
-        // third needs 6: 80 VGPRs), so it takes the spill-free target of 4
-        constexpr int wpe = I.pairs == kWide4 ? 4
-                            : sizeof(T) == 8 ? net_wpe(bytes, kProgWpeMax, kNTof<I.pairs> / 64)
-                                             : (I.dual ? 4 : 5);
+        constexpr int wpe = sizeof(T) == 8 ? net_wpe(bytes, kProgWpeMax, kNTof<I.pairs> / 64)
+                                           : (I.dual ? 4 : 5);
         return (const void*)net_kernel<T, false, I.dual != 0, wpe, I.pairs, PID>;
     }
 }
@@ -1427,10 +1396,10 @@ const void* prog_fn(int pid) {
     }
 }
 
-// threads of a workgroup of pairs code np (kNTof at run time)
-int net_threads(int np) { return np == 2 ? kNTof<2> : np == kWide4 ? kNTof<kWide4> : kNT; }
-// pair units (arenas) a workgroup of pairs code np holds
-int net_units(int np) { return np == 2 ? kUnitsOf<2> : np == kWide4 ? kUnitsOf<kWide4> : np; }
+// threads of a workgroup of np pairs (kNTof at run time)
+int net_threads(int np) { return np == 2 ? kNTof<2> : kNT; }
+// pair units (arenas) a workgroup of np pairs holds
+int net_units(int np) { return np == 2 ? kUnitsOf<2> : np; }
 
 int net_occupancy(const void* fn, int lds_bytes, int threads) {
     if (lds_bytes > 64 * 1024 &&
@@ -1579,21 +1548,17 @@ int net_impl(const cgp_net_args* a, void* stream) {
     p.part = a->part;
     p.lds_elems = a->lds_elems;
     p.exact = (a->flags & CGP_FLAG_EXACT_RELU) ? 1 : 0;
-    const int np = a->pairs <= 0 ? 1 : a->pairs;   // the pairs code
-    if (np != 1 && np != 2 && np != 4 && np != kMaxNP && np != kWide4)
-        return fail(CGP_EINVAL, "net: pairs code %d (1, 2, 4, 16 or CGP_NET_PAIRS_WIDE4)", np);
-    if (np == kWide4 && a->program <= 0)
-        return fail(CGP_EINVAL, "net: a wide stage runs a compiled program only");
+    const int np = a->pairs <= 0 ? 1 : a->pairs;
+    if (np != 1 && np != 2 && np != 4 && np != kMaxNP)
+        return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 2, 4 or 16)", np);
     if (lds_bytes * net_units(np) > 160 * 1024)
         return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * net_units(np));
-    // multi-pair stages address a pair's variance maps (<= 8 * threads / pairs pixels) with
-    // 32-bit byte offsets (VarSrc), a wide stage's moments also the pair's images
-    const long long nmax = a->n1 > a->n2 ? a->n1 : a->n2;
-    if (np > 1 && nmax * (8LL * net_threads(np) / net_units(np)) * (long long)sizeof(T) >=
-                          (1LL << 32))
-        return fail(CGP_EINVAL, "net: %lld images too many for pairs code %d", nmax, np);
-    if (np == kWide4 && nmax * a->channels * a->h * a->w * (long long)sizeof(T) >= (1LL << 32))
-        return fail(CGP_EINVAL, "net: %lld images too large for a wide stage", nmax);
+    // multi-pair stages address a pair's variance maps (<= 8 * threads / np pixels) with
+    // 32-bit byte offsets (VarSrc)
+    if (np > 1 && (a->n1 > a->n2 ? a->n1 : a->n2) * (8LL * net_threads(np) / np) *
+                          (long long)sizeof(T) >= (1LL << 32))
+        return fail(CGP_EINVAL, "net: %lld images too many for %d pairs per workgroup",
+                    (long long)(a->n1 > a->n2 ? a->n1 : a->n2), np);
     if (a->unit_begin == 0 && a->unit_end == 0) {
         p.ubeg = 0;
         p.uend = p.units;
@@ -1601,7 +1566,7 @@ int net_impl(const cgp_net_args* a, void* stream) {
         p.ubeg = a->unit_begin;
         p.uend = a->unit_end;
     }
-    if (p.ubeg < 0 || p.uend > p.units || p.ubeg >= p.uend || p.ubeg % net_units(np))
+    if (p.ubeg < 0 || p.uend > p.units || p.ubeg >= p.uend || p.ubeg % np)
         return fail(CGP_EINVAL, "net: unit range [%lld, %lld) of %lld", (long long)p.ubeg,
                     (long long)p.uend, (long long)p.units);
     p.final_stage = a->final_stage;
@@ -1648,7 +1613,6 @@ int cgp_net_hs_elems(int32_t code) {
 
 int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs) {
     if (pairs <= 0) pairs = 1;
-    if (pairs == kWide4) return 0;   // compiled programs only: no interpreter instantiation
     if (lds_bytes <= 0 || (long long)lds_bytes * pairs > 160 * 1024) return 0;
     return f64 ? net_occupancy_for<double>(lds_bytes, flags, pairs)
                : net_occupancy_for<float>(lds_bytes, flags, pairs);

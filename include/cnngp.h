@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 9
+#define CGP_ABI_VERSION 8
 
 /* error codes */
 #define CGP_OK 0
@@ -265,10 +265,6 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
  * first cells: separable row passes write their input rows there and a one-pair
  * full-map reduction its two wave partial sums. */
 #define CGP_NET_CODE_HS_CLEAN 0x100
-/* cgp_net_args.pairs: four pairs on 448 threads (seven waves) — a 28x28 pass's 4 x 112
- * items of 7 outputs fill every lane, where a pair on 128 threads leaves 16 idle.
- * Compiled programs only (cgp_net_program with this code); ABI 9. */
-#define CGP_NET_PAIRS_WIDE4 0x104
 
 typedef struct cgp_net_op {
     int32_t kind;          /* CGP_NET_* */
@@ -313,7 +309,7 @@ typedef struct cgp_net_args {
     int32_t pairs;         /* pairs per workgroup: 1; 2 = two one-pair slices of a 256-thread
                               workgroup (units u, u + 1: the same image i), any op list; or
                               4 / 16 for a stage whose maps are at most 16x16 / 8x8 (each
-                              pair gets its own lds_elems arena); or CGP_NET_PAIRS_WIDE4 */
+                              pair gets its own lds_elems arena) */
     int64_t unit_begin;    /* the tile's pair units this launch covers, [begin, end): unit */
     int64_t unit_end;      /* u = 64·supertile + 8·(i % 8) + j % 8; 0, 0 = the whole tile */
     int32_t final_stage;   /* 1: write K (the last stage); 0: the ops end in CGP_NET_STORE */

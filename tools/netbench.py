@@ -119,17 +119,12 @@ def main():
             per = {}
             for pairs_, e0, e1 in ev:
                 per[pairs_] = per.get(pairs_, 0.0) + e0.elapsed_time(e1)
-            print("   per stage (ms): " + "  ".join(
-                f"{lib.cgp_net_units(k)}p{'/448t' if k == N.CGP_NET_PAIRS_WIDE4 else ''} {v:.2f}"
-                for k, v in per.items()))
+            print("   per stage (ms): " + "  ".join(f"{k}p {v:.2f}" for k, v in per.items()))
         it = X.element_size()
-        def label(st):
-            u = lib.cgp_net_units(st.pairs)
-            wide = st.pairs == N.CGP_NET_PAIRS_WIDE4
-            occ = "" if wide else (" occ(interp)=" + str(lib.cgp_net_occupancy(
-                st.lds_elems * it, int(dt == torch.float64), 4 if st.dual else 0, st.pairs)))
-            return f"[{u}p{'/448t' if wide else ''} {st.n_ops}ops {st.lds_elems * it * u}B{occ}]"
-        stages = " ".join(label(st) for st in net.stages)
+        stages = " ".join(
+            f"[{st.pairs}p {st.n_ops}ops {st.lds_elems * it * st.pairs}B "
+            f"occ(interp)={lib.cgp_net_occupancy(st.lds_elems * it, int(dt == torch.float64), 4 if st.dual else 0, st.pairs)}]"
+            for st in net.stages)
         print(f"{name:28s} net {ms_net:8.2f} ms ({pairs / ms_net / 1e3:7.2f} M pairs/s)  "
               f"forward {ms_fwd:8.2f} ms  {stages}")
 
