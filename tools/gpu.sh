@@ -20,7 +20,8 @@
 #   py:SCRIPT     python SCRIPT (a probe under tools/)
 #   ab            netbench (NB_ARGS) for each build in $AB: "cur" = lib/libcnngp.so, any other
 #                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds;
-#                 AB_TEST=1 runs each variant's whole-network parity tests first; a NAME=VALUE
+#                 AB_TEST=1 runs each variant's whole-network parity tests first; AB_TOOL
+#                 times another script (e.g. tools/stencil_once.py); a NAME=VALUE
 #                 entry runs the current library with that environment variable
 #   envtest       pytest $PYTEST_ARGS with the environment ENVTEST="NAME=VALUE ..."
 set -u
@@ -106,7 +107,7 @@ for s in "${LIST[@]}"; do
                 *) lib=$PWD/cnn-gp_amd/lib/ab/lib_$v.so ;;
                 esac
                 env $envset CNNGP_LIB=$lib bash -c "$(declare -f step); O=$O; \
-                    step ab_${tag}_$rep 300 python tools/netbench.py ${NB_ARGS:-}" || exit 1
+                    step ab_${tag}_$rep 300 python ${AB_TOOL:-tools/netbench.py} ${NB_ARGS:-}" || exit 1
                 echo "-- $v (round $rep)"; grep -v amdgpu.ids "$O/ab_${tag}_$rep.log" | tail -n 8
             done
         done ;;
