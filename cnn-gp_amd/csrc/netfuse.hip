@@ -1473,20 +1473,9 @@ unsigned long long* work_counters(hipStream_t s) {
 template <typename T>
 int net_launch(const NetP<T>& p, bool ex, bool du, int np, long long lds_bytes, int program,
                void* stream) {
-    long long wg_bytes = lds_bytes * net_units(np);
+    const long long wg_bytes = lds_bytes * net_units(np);
     const void* fn = program > 0 && !ex ? prog_fn<T>(program - 1) : net_fn<T>(ex, du, np, wg_bytes);
     if (!fn) return fail(CGP_EINVAL, "net: no instantiation for %d pairs per workgroup", np);
-    // occupancy probe (diagnostic, round 4): CGP_NET_MAX_WG=N reserves enough LDS that at
-    // most N two-pair head workgroups fit a CU
-    if (np == 2) {
-        if (const char* cap = getenv("CGP_NET_MAX_WG")) {
-            const long long n = atoll(cap);
-            if (n > 0 && wg_bytes <= 163840 / n) {
-                const long long pad = 163840 / (n + 1) + 256;
-                if (pad > wg_bytes && pad <= 163840 / n) wg_bytes = pad;
-            }
-        }
-    }
     const int per_cu = net_occupancy(fn, (int)wg_bytes, net_threads(np));
     if (per_cu <= 0)
         return fail(CGP_EINVAL, "net: kernel cannot be resident with %lld B LDS", wg_bytes);

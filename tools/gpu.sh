@@ -16,7 +16,6 @@
 #   trace:CFG     rocprofv3 --kernel-trace --stats over bench.py --config CFG
 #   pmc           PMC passes (tools/pmc.sh; PMC_CFGS) summarised into $O/net_pmc.json
 #   fullscale     tools/fullscale.py $FS_ARGS
-#   occ           netbench (NB_ARGS) with CGP_NET_MAX_WG = each of OCC_CAPS (0 = uncapped)
 #   py:SCRIPT     python SCRIPT (a probe under tools/)
 #   ab            netbench (NB_ARGS) for each build in $AB: "cur" = lib/libcnngp.so, any other
 #                 name = cnn-gp_amd/lib/ab/lib_NAME.so (tools/build_variant.sh); AB_REPS rounds;
@@ -117,17 +116,6 @@ for s in "${LIST[@]}"; do
             pytest ${PYTEST_ARGS:-tests/test_gpu_parity.py} -x -q --timeout 300 \
             --timeout-method thread" || exit 1
         tail -n 1 "$O/envtest.log" ;;
-    occ)
-        # head-stage occupancy probe: CGP_NET_MAX_WG caps the two-pair workgroups per CU
-        for rep in 1 2; do
-            for cap in ${OCC_CAPS:-0 5 4 3}; do
-                if [ "$cap" = 0 ]; then unset CGP_NET_MAX_WG; else export CGP_NET_MAX_WG=$cap; fi
-                step "occ_${cap}_$rep" 300 python tools/netbench.py ${NB_ARGS:-}
-                echo "-- max workgroups per CU: $cap (round $rep)"
-                grep -v amdgpu.ids "$O/occ_${cap}_$rep.log" | tail -n 8
-            done
-        done
-        unset CGP_NET_MAX_WG ;;
     py:*)
         p=${s#py:}
         step "py_$(basename "$p" .py)" 600 python "$p" ${PY_ARGS:-}
