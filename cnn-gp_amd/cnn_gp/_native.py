@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 8
+CGP_ABI_VERSION = 9
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -23,6 +23,9 @@ CGP_POST_NONE, CGP_POST_RELU = 0, 1
 CGP_NET_CONV, CGP_NET_RELU, CGP_NET_MOMENTS, CGP_NET_LINEAR = 0, 1, 2, 3
 CGP_NET_LOAD, CGP_NET_STORE = 4, 5
 CGP_NET_CODE_HS_CLEAN = 0x100
+CGP_NET_CODE_SUM = 0x200         # conv: outputs summed for the next op's reduction (cnngp.h)
+CGP_NET_CODE_FROM_SUM = 0x400    # reduction: reads the previous conv's partial sums
+CGP_NET_CODE_GEOMETRY = 0xff
 CGP_VAR_MOMENTS, CGP_VAR_CONV, CGP_VAR_HALF, CGP_VAR_SUM = 0, 1, 2, 3
 
 _vp = ctypes.c_void_p

@@ -45,6 +45,11 @@ TIMING = None
 # the reference configs' lowered programs, every offset an immediate).  False forces the
 # op-record interpreter (A/B and parity tests of both paths).
 USE_PROGRAMS = os.environ.get("CGP_NET_PROGRAMS", "1") != "0"
+# a separable conv whose map only the next op's full-map reduction reads keeps its outputs
+# in registers and hands the reduction its wave partial sums (cnngp.h CGP_NET_CODE_SUM /
+# CGP_NET_CODE_FROM_SUM; one pair per workgroup or half): no map store, no map re-read,
+# one barrier less per pair.  CGP_NET_FUSE_REDUCE=0 keeps the two ops apart.
+FUSE_REDUCE = os.environ.get("CGP_NET_FUSE_REDUCE", "1") != "0"
 # quartered x-side variance maps for the fp64 closed-form ReLU (relu_q_n); 0 only to time
 # library builds that predate it (tools/variants.sh)
 QUARTER_MAPS = os.environ.get("CGP_NET_QUARTER", "1") != "0"
@@ -496,6 +501,7 @@ class NetPlan:
             recs = folded
         hs_part = self._reduce_cells(recs)
         self._mark_hs_clean(recs, pairs, hs_part)
+        self._fuse_reductions(recs, pairs)
         for f, _ in recs:
             # (a two-pair stage runs its ops as one-pair halves: lowered like one pair)
             if f["kind"] == N.CGP_NET_RELU or (f["kind"] == N.CGP_NET_LINEAR and pairs > 2):
@@ -515,7 +521,7 @@ class NetPlan:
         outside the input are zero rows), or None for a conv without scratch (1x1,
         full-map reduction, single-pass <= 3 taps: cgp_net_hs_elems() <= 2)."""
         h, w, ho, wo, taps, s, off = f["geom"]
-        hs_elems = self._lib.cgp_net_hs_elems(f["code"] & (N.CGP_NET_CODE_HS_CLEAN - 1))
+        hs_elems = self._lib.cgp_net_hs_elems(f["code"] & N.CGP_NET_CODE_GEOMETRY)
         if hs_elems <= 2:
             return None
         hsr = (ho - 1) * s + taps
@@ -537,6 +543,32 @@ class NetPlan:
                     data = cells[1]
                     lo, hi = max(lo, min(data)), min(hi, max(data) + 1)
         return lo if lo + 2 <= hi else 0
+
+    @staticmethod
+    def _fuse_reductions(recs, pairs):
+        """CGP_NET_CODE_SUM on a separable conv (no addend, no second output) whose map is
+        read only by the next record, a full-map reduction, which gets
+        CGP_NET_CODE_FROM_SUM (one pair per workgroup or half only)."""
+        if pairs > 2 or not FUSE_REDUCE:
+            return
+        for k in range(len(recs) - 1):
+            f, g = recs[k][0], recs[k + 1][0]
+            if f["kind"] != N.CGP_NET_CONV or g["kind"] != N.CGP_NET_CONV:
+                continue
+            h, w, ho, wo, taps, s_, off = f["geom"]
+            point = taps == 1 and off == 0
+            full = ho == wo == 1 and off == 0 and taps == h == w
+            if taps <= 3 or point or full or f.get("dst2", -1) >= 0 or f["add"] >= 0:
+                continue
+            gh, gw, gho, gwo, gtaps, _, goff = g["geom"]
+            if not (gho == gwo == 1 and goff == 0 and gtaps == gh == gw) or g["src"] != f["dst"]:
+                continue
+            slot = f["dst"]
+            if any(r["src"] == slot or r["add"] == slot or r.get("dst2", -1) == slot
+                   for r, _ in recs[k + 2:]):
+                continue
+            f["code"] |= N.CGP_NET_CODE_SUM
+            g["code"] |= N.CGP_NET_CODE_FROM_SUM
 
     def _mark_hs_clean(self, recs, pairs, hs_part=0):
         """CGP_NET_CODE_HS_CLEAN on every separable conv whose zero rows of the row-sum

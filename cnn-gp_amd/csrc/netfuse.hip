@@ -260,6 +260,7 @@ struct Pairs {
     unsigned i, j;
     const unsigned* tab;
     long long u0;
+    void* red;   // one-pair code: the pair's two wave partial sums (CGP_NET_CODE_SUM)
 };
 template <int NP>
 __device__ __forceinline__ void pair_q(const Pairs& pr, int q, unsigned& iq, unsigned& jq) {
@@ -498,20 +499,25 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
 
     if constexpr (G::REDUCE && NP == 1) {
         prio_alu<NP, G::HW>();
-        // 1x1 output from a full-plane window: a block reduction
-        T acc = T(0);
+        // 1x1 output from a full-plane window: a block reduction — or, after a conv marked
+        // CGP_NET_CODE_SUM, the wave partial sums that conv left (the map was never stored)
+        const bool from_sum = (op.code & CGP_NET_CODE_FROM_SUM) != 0;
+        T* part = from_sum ? static_cast<T*>(pr.red)
+                           : lds + p.part;   // off the scratch's zero rows (cgp_net_args.part)
+        if (!from_sum) {
+            T acc = T(0);
 #pragma unroll
-        for (int k = 0; k < (G::HW + G::NT - 1) / G::NT; ++k) {
-            const int px = tid + k * G::NT;
-            if (G::HW % G::NT == 0 || px < G::HW) {
-                const int r = udiv(px, G::W), c = px - r * G::W;
-                acc += src[r * wsi + c];
+            for (int k = 0; k < (G::HW + G::NT - 1) / G::NT; ++k) {
+                const int px = tid + k * G::NT;
+                if (G::HW % G::NT == 0 || px < G::HW) {
+                    const int r = udiv(px, G::W), c = px - r * G::W;
+                    acc += src[r * wsi + c];
+                }
             }
+            acc = wave_sum(acc);
+            if ((tid & 63) == 0) part[tid >> 6] = acc;
+            lds_barrier();
         }
-        acc = wave_sum(acc);
-        T* part = lds + p.part;   // off the scratch's zero rows (cgp_net_args.part)
-        if ((tid & 63) == 0) part[tid >> 6] = acc;
-        lds_barrier();
         if (tid == 0) {
             T tot = part[0];
 #pragma unroll
@@ -717,7 +723,11 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         }
         lds_barrier();
         // column pass + output stage (uniform branches outside the per-pixel loops: each
-        // stage is one basic block, so the R3 independent ReLUs interleave)
+        // stage is one basic block, so the R3 independent ReLUs interleave).  A conv marked
+        // CGP_NET_CODE_SUM (one pair) keeps its outputs in registers and leaves only their
+        // wave sums for the reduction that follows
+        const bool to_sum = NP == 1 && (op.code & CGP_NET_CODE_SUM) != 0;
+        T sacc = T(0);
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * G::NT;
@@ -744,8 +754,22 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
                     at[k] = q * arena + (g3 * G::R3 + k) * wso + c;
                     ok[k] = true;
                 }
-                net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, v, at, ok, u1[kv], u2[kv], tab,
-                                                        NP == 1 ? ~0ull : vote_lanes<G::NV, NP>(it));
+                if (to_sum) {
+                    if (op.relu) relu_n<EX, kQuarter<T, EX>, T, G::R3, 1>(v, u1[kv], u2[kv], tab);
+#pragma unroll
+                    for (int k = 0; k < G::R3; ++k) sacc += v[k];
+                } else {
+                    net_out<T, EX, DU, G::R3, kAdaptOf<NP>>(lds, op, v, at, ok, u1[kv], u2[kv],
+                                                            tab,
+                                                            NP == 1 ? ~0ull
+                                                                    : vote_lanes<G::NV, NP>(it));
+                }
+            }
+        }
+        if constexpr (NP == 1) {
+            if (to_sum) {
+                sacc = wave_sum(sacc);
+                if ((tid & 63) == 0) static_cast<T*>(pr.red)[tid >> 6] = sacc;
             }
         }
     }
@@ -1004,7 +1028,7 @@ __device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op
     }
     switch (op.kind) {
     case CGP_NET_CONV:
-        switch (op.code & (CGP_NET_CODE_HS_CLEAN - 1)) {
+        switch (op.code & CGP_NET_CODE_GEOMETRY) {
             CGP_NET_GEOMETRIES(CGP_NET_CASE)
         default:
             break;
@@ -1093,7 +1117,7 @@ __device__ __forceinline__ cgp_net_op prog_op(const ProgRec* recs) {
 template <int PID, int K, int NP>
 struct ProgGeo {
     static constexpr ProgOp o = kProgOps[kProgs[PID].first + K];
-    static constexpr GeoRow g = kGeoTable[o.code & (CGP_NET_CODE_HS_CLEAN - 1)];
+    static constexpr GeoRow g = kGeoTable[o.code & CGP_NET_CODE_GEOMETRY];
     using G = NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>;
 };
 template <typename T, bool DU, int NP, int PID, int K>
@@ -1160,6 +1184,7 @@ template <typename T, bool EX, bool DU, int WPE, int NP, int PID = -1>
 __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))) void net_kernel(const NetP<T> p) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     __shared__ unsigned pair_tab[2 * kMaxNP];
+    __shared__ T red_part[kUnitsOf<NP> * (kNT / 64)];   // CGP_NET_CODE_SUM partials
     T* lds = reinterpret_cast<T*>(smem_raw);
     const int tid = threadIdx.x;
     constexpr int UN = kUnitsOf<NP>;
@@ -1203,6 +1228,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
+        pr.red = red_part;
         if constexpr (NP == 2) {
             // one-pair slices sharing the workgroup's barriers: waves 2q, 2q + 1 run unit
             // u + q (the next j of the same image i), each on its own arena.  The pair is
@@ -1234,6 +1260,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             Pairs ph;
             ph.tab = pair_tab;
             ph.u0 = u + q;
+            ph.red = red_part + q * (kNT / 64);
             // a slice without a pair computes on clamped indices and stores nothing
             ph.i = __builtin_amdgcn_readfirstlane(vq ? iq : 0u);
             ph.j = __builtin_amdgcn_readfirstlane(vq ? jq : 0u);

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 8
+#define CGP_ABI_VERSION 9
 
 /* error codes */
 #define CGP_OK 0
@@ -265,11 +265,21 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
  * first cells: separable row passes write their input rows there and a one-pair
  * full-map reduction its two wave partial sums. */
 #define CGP_NET_CODE_HS_CLEAN 0x100
+/* CONV code flags of a map that only a full-map reduction reads (ABI 9; one pair per
+ * workgroup or half; the host sets both or neither):
+ *   CGP_NET_CODE_SUM       a separable conv does not store its output map: each wave adds
+ *                          its outputs (after the ReLU) into the pair's two wave partial sums
+ *   CGP_NET_CODE_FROM_SUM  the next op, a full-map reduction (1x1 output, window = map) of
+ *                          that map, reads those partial sums instead of the map */
+#define CGP_NET_CODE_SUM 0x200
+#define CGP_NET_CODE_FROM_SUM 0x400
+#define CGP_NET_CODE_GEOMETRY 0xff  /* the cgp_net_geometry() code in the low bits */
 
 typedef struct cgp_net_op {
     int32_t kind;          /* CGP_NET_* */
     int32_t code;          /* CONV: cgp_net_geometry(), | CGP_NET_CODE_HS_CLEAN when the row
-                              sums' zero rows are known to be zero already;
+                              sums' zero rows are known to be zero already, | CGP_NET_CODE_SUM
+                              / CGP_NET_CODE_FROM_SUM for a map only a reduction reads;
                               RELU/LINEAR/MOMENTS: cgp_net_resolution() of the map, or -1
                               (generic) */
     int32_t src, dst, add; /* LDS element offsets of the slots' (0, 0) pixel; add < 0: none */

@@ -16,6 +16,8 @@ from oracle import nngp_oracle as O
 
 TINY = O.F32_TINY
 HS_CLEAN = 0x100            # cgp_net_op.code flag (include/cnngp.h CGP_NET_CODE_HS_CLEAN)
+SUM, FROM_SUM = 0x200, 0x400  # CGP_NET_CODE_SUM / CGP_NET_CODE_FROM_SUM
+GEOMETRY = 0xff
 
 
 def _conv_maps(m, geom, weight, bias):
@@ -72,6 +74,7 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
     stale values of earlier pairs stay in every cell an op does not write — as on the
     device.  ``state``: {"in": record, "out": record} of this pair's unit."""
     hs0 = 0
+    fused = None               # the map sum a CGP_NET_CODE_SUM conv hands the next reduction
 
     def plane(off, h, w, ws):
         idx = off + np.arange(h)[:, None] * ws + np.arange(w)[None, :]
@@ -133,8 +136,12 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
             out = np.zeros((ho, wo))
             for r in range(ho):
                 out[r] = hs[r * s:r * s + taps].sum(0)
+            if f["code"] & FROM_SUM:
+                # the previous conv's outputs were never stored: its sums stand for the map
+                assert reduce and fused is not None
+                out = np.full((1, 1), fused)
             out = f["weight"] * out + f["bias"]
-            if reduce and stage.pairs <= 2:
+            if reduce and stage.pairs <= 2 and not f["code"] & FROM_SUM:
                 # a one-pair reduction leaves its two wave partial sums at cgp_net_args.part
                 flat = src.reshape(-1)
                 lds[stage.part] = flat[np.arange(flat.size) % 128 < 64].sum() + 1.0
@@ -142,6 +149,10 @@ def run_stage(stage, x_i, y_j, var, i, j, lds, state):
             if f.get("relu"):
                 vx, vy = var[v]
                 out = _relu(out, vx[i], vy[j])
+            if f["code"] & SUM:                                 # kept in registers
+                assert f["add"] < 0 and f.get("dst2", -1) < 0
+                fused = out.sum()
+                continue
             if f["add"] >= 0:
                 out = out + lds[plane(f["add"], ho, wo, f["ws_out"])]
             lds[plane(f["dst"], ho, wo, f["ws_out"])] = out
