@@ -1120,32 +1120,6 @@ struct ProgGeo {
     static constexpr GeoRow g = kGeoTable[o.code & CGP_NET_CODE_GEOMETRY];
     using G = NG<g.h, g.w, g.ho, g.wo, g.taps, g.s, g.off, NP>;
 };
-#ifndef CGP_NET_TAIL_BARRIERS
-#define CGP_NET_TAIL_BARRIERS 0
-#endif
-// The barrier after op K of a program.  Not needed when no later LDS access of this pair
-// depends on op K: op K is the last op and only reads LDS (a STORE to the state record) or
-// hands its one value to the same thread (a one-pair reduction from CGP_NET_CODE_SUM
-// partials: thread 0 of the half writes the final slot and reads it for K), or ops K and
-// K + 1 are both STOREs (they only read LDS).  The pair walk's own barrier (advance) orders
-// this pair's last LDS reads before the next pair's first writes.
-template <int PID, int K, int NP>
-constexpr bool prog_barrier_after() {
-    if constexpr (CGP_NET_TAIL_BARRIERS) {
-        return true;
-    } else {
-        constexpr ProgInfo I = kProgs[PID];
-        constexpr ProgOp o = kProgOps[I.first + K];
-        constexpr bool store = o.kind == CGP_NET_STORE;
-        if constexpr (K + 1 == I.nops) {
-            return !(store || (NP == 1 && o.kind == CGP_NET_CONV &&
-                               (o.code & CGP_NET_CODE_FROM_SUM) != 0));
-        } else {
-            return !(store && kProgOps[I.first + K + 1].kind == CGP_NET_STORE);
-        }
-    }
-}
-
 template <typename T, bool DU, int NP, int PID, int K>
 __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, const Pairs& pr,
                                          int tid, const ProgRec* recs) {
@@ -1172,7 +1146,7 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
         } else if constexpr (o.kind == CGP_NET_LOAD || o.kind == CGP_NET_STORE) {
             net_move<T, o.kind, NP>(lds, op, p, pr);
         }
-        if constexpr (prog_barrier_after<PID, K, NP>()) lds_barrier();
+        lds_barrier();
         prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid, recs);
     }
 }
@@ -1362,9 +1336,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
                 }
             }
         }
-        // (no barrier here: the next advance() is one, and it follows every LDS read of
-        // this pair — the last op's own barrier made its results visible)
-        if constexpr (CGP_NET_TAIL_BARRIERS) lds_barrier();
+        lds_barrier();
     }
 }
 
