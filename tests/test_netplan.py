@@ -70,3 +70,33 @@ def test_slot_reuse_is_tight():
                or f["kind"] == 0 and f.get("geom", (0,) * 7)[2] == 28})
     assert n28 <= 3
     assert ws == 29                             # 28 + one shared zero column
+
+
+@pytest.mark.parametrize("cfg,fused", [("mnist_paper_convnet_gp", True),
+                                       ("mnist_paper_residual_cnn_gp", True),
+                                       ("mnist_as_tf", False), ("cifar10", False)])
+def test_conv_fused_into_final_reduction(cfg, fused, monkeypatch):
+    """the separable conv whose map only the full-map reduction reads is marked SUM and the
+    reduction FROM_SUM (one-pair stages only; the ResNets reduce in a 16-pair stage after a
+    conv with an addend); CGP_NET_FUSE_REDUCE=0 keeps them apart, emulated results agree"""
+    from cnn_gp import _native as N
+    from cnn_gp import netplan
+    C, side = specs.GEOMETRY[cfg]
+    m = configs_util.model(cfg)
+    net = NetPlan(Plan(m, side, side))
+    codes = [f["code"] for f, _ in net.records if f["kind"] == N.CGP_NET_CONV]
+    n_sum = sum(1 for c in codes if c & N.CGP_NET_CODE_SUM)
+    n_from = sum(1 for c in codes if c & N.CGP_NET_CODE_FROM_SUM)
+    assert (n_sum, n_from) == ((1, 1) if fused else (0, 0))
+    if fused:
+        k = next(k for k, (f, _) in enumerate(net.records)
+                 if f["kind"] == N.CGP_NET_CONV and f["code"] & N.CGP_NET_CODE_SUM)
+        assert net.records[k + 1][0]["code"] & N.CGP_NET_CODE_FROM_SUM
+        monkeypatch.setattr(netplan, "FUSE_REDUCE", False)
+        apart = NetPlan(Plan(m, side, side))
+        assert not any(f["code"] & (N.CGP_NET_CODE_SUM | N.CGP_NET_CODE_FROM_SUM)
+                       for f, _ in apart.records if f["kind"] == N.CGP_NET_CONV)
+        rng = np.random.default_rng(8)
+        X = rng.random((3, C, side, side))
+        np.testing.assert_allclose(E.kernel(net, X, X, True), E.kernel(apart, X, X, True),
+                                   rtol=1e-14)
