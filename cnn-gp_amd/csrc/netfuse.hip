@@ -130,12 +130,11 @@ constexpr GeoRow kGeoTable[] = {CGP_NET_GEOMETRIES(CGP_NET_ROW)};
 constexpr int kNumGeo = sizeof(kGeoTable) / sizeof(kGeoTable[0]);
 
 // out[o] = Σ_{t<TAPS} w[o·S + t], o < R.  Stride 1 with TAPS ≥ 4: outputs in groups of
-// g ≤ TAPS share the common core of their windows; the left parts are suffix sums and
-// the right parts prefix sums, so a group costs TAPS + 3g - 6 adds instead of g(TAPS-1)
-// (TAPS + 2g - 4 with the suffix sums run through the core, CGP_NET_WIN_VH).
-#ifndef CGP_NET_WIN_VH
-#define CGP_NET_WIN_VH 1
-#endif
+// g ≤ TAPS share the common core of their windows; the suffix sums of the first window run
+// through the core and the taps after it are prefix sums, so a group costs TAPS + 2g - 4
+// adds instead of g(TAPS-1) (7x7: 17 per pass instead of 42).  The round-3 form kept the
+// core apart (TAPS + 3g - 6: 22) and measured 2.5% slower on ConvNet GP
+// (profiles/r4/ab_r4l_window_sums.log).
 template <typename T, int TAPS, int O0, int G, int N, int R>
 __device__ __forceinline__ void win_group(const T (&w)[N], T (&out)[R]) {
     T core = w[O0 + G - 1];
@@ -143,7 +142,7 @@ __device__ __forceinline__ void win_group(const T (&w)[N], T (&out)[R]) {
     for (int t = O0 + G; t < O0 + TAPS; ++t) core += w[t];
     if constexpr (G == 1) {
         out[O0] = core;
-    } else if constexpr (CGP_NET_WIN_VH) {
+    } else {
         // suffix sums of the first window that end in the core, prefix sums of the taps
         // after it (van Herk / Gil-Werman): TAPS + 2G - 4 adds
         T suf[G], right[G];
@@ -156,18 +155,6 @@ __device__ __forceinline__ void win_group(const T (&w)[N], T (&out)[R]) {
         out[O0] = suf[0];
 #pragma unroll
         for (int o = 1; o < G; ++o) out[O0 + o] = suf[o] + right[o];
-    } else {
-        T left[G], right[G];
-        left[G - 2] = w[O0 + G - 2];
-#pragma unroll
-        for (int o = G - 3; o >= 0; --o) left[o] = w[O0 + o] + left[o + 1];
-        right[1] = w[O0 + TAPS];
-#pragma unroll
-        for (int o = 2; o < G; ++o) right[o] = right[o - 1] + w[O0 + TAPS + o - 1];
-        out[O0] = left[0] + core;
-#pragma unroll
-        for (int o = 1; o < G - 1; ++o) out[O0 + o] = (left[o] + core) + right[o];
-        out[O0 + G - 1] = core + right[G - 1];
     }
 }
 
