@@ -114,6 +114,7 @@ def make_fastdiv(d: int):
 # name -> (restype, argtypes)
 SIGNATURES = {
     "cgp_abi_version": (_i32, []),
+    "cgp_net_xvar_scale": (ctypes.c_double, []),
     "cgp_last_error": (ctypes.c_char_p, []),
     "cgp_conv_args_size": (ctypes.c_size_t, []),
     "cgp_relu_args_size": (ctypes.c_size_t, []),

@@ -716,7 +716,8 @@ class NetPlan:
 
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2
 
-        if quarters:   # one launch fills every quartered map
+        if quarters:   # one launch fills every scaled map (cgp_net_xvar_scale: 1/16)
+            xscale = lib.cgp_net_xvar_scale()
             nq = len(quarters)
             q_src = (ctypes.c_void_p * nq)(*[N.ptr(s_) for s_, _ in quarters])
             q_dst = (ctypes.c_void_p * nq)(*[N.ptr(q_) for _, q_ in quarters])
@@ -724,7 +725,7 @@ class NetPlan:
 
         def run_all(stream):
             if quarters:
-                N.call("cgp_scale_batch_f64", nq, q_src, q_dst, q_n, 0.25, stream)
+                N.call("cgp_scale_batch_f64", nq, q_src, q_dst, q_n, xscale, stream)
             for u0 in range(0, units, chunk):
                 u1 = min(units, u0 + chunk)
                 for a in launches:

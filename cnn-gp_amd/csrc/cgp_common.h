@@ -163,8 +163,17 @@ __device__ __forceinline__ float fma_t(float a, float b, float c) {
 // v_fma_f64 with an SGPR-pair operand and the table lives in SGPRs only while in use.
 // P̃(x4) = P(x4/4)/16: coefficient k scaled by 1/(16·4^k), exact powers of two, so Horner in
 // x4 = 4x rounds exactly like Horner in x (relu_q_n)
+// x-side variance maps the fp64 closed form reads: v / 2^CGP_XVAR_SHIFT (exact).  4 (1/16,
+// ABI 9): its Newton step then yields y = 8/sqrt(t), so u = 4x = 2 - |c/4|·y is one fma with
+// source modifiers, sqrt(t)/2 comes out of the same step and the polynomial's coefficients
+// carry the factor 2 back (exact); 2 (1/4, rounds 2-3) needs a multiply and a min for u
+#ifndef CGP_XVAR_SHIFT
+#define CGP_XVAR_SHIFT 4
+#endif
+constexpr double kXVarScale = CGP_XVAR_SHIFT == 4 ? 0.0625 : 0.25;
+constexpr double kPolyQ = CGP_XVAR_SHIFT == 4 ? 0.125 : 0.0625;   // P̃ = P(x4/4)·kPolyQ
 constexpr double poly_q(int k) {
-    double v = kReluPolyD[k] * 0.0625;
+    double v = kReluPolyD[k] * kPolyQ;
     for (int n = 0; n < k; ++n) v *= 0.25;
     return v;
 }
@@ -195,7 +204,7 @@ template <int D>
 constexpr AdaptCoef<D> adapt_coef(const double (&p)[D + 1]) {
     AdaptCoef<D> t{};
     for (int k = 0; k <= D; ++k) {
-        double v = p[k] * 0.0625;
+        double v = p[k] * kPolyQ;
         for (int n = 0; n < k; ++n) v *= 0.25;
         t.c[k] = v;
     }
@@ -325,17 +334,22 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if constexpr (!QIN) c[r] *= 0.25;
-        const double T = __builtin_fma(v1q[r], v2[r], 0.25 * K<double>::tiny);
+        const double T = __builtin_fma(v1q[r], v2[r], kXVarScale * K<double>::tiny);
         const double r0 = __builtin_amdgcn_rsq(T);
         const double m = T * r0;
         const double k = __builtin_fma(-m, r0, 3.0);
-        y[r] = r0 * k;
-        st[r] = m * k;
+        y[r] = r0 * k;      // 4/sqrt(t) (shift 2) or 8/sqrt(t) (shift 4)
+        st[r] = m * k;      // sqrt(t) or sqrt(t)/2
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const double a = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);
-        u[r] = __builtin_fma(-2.0, a, 2.0);
+        if constexpr (CGP_XVAR_SHIFT == 4) {
+            // u = 2 - 2|rho| in one rounding, floored at 2^-51 (|rho| <= 1 - 2^-52 as below)
+            u[r] = __builtin_fmax(__builtin_fma(-__builtin_fabs(c[r]), y[r], 2.0), 2.0 - 2.0 * kRhoMax);
+        } else {
+            const double a = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);
+            u[r] = __builtin_fma(-2.0, a, 2.0);
+        }
         const double h = __builtin_amdgcn_rsq(u[r]);
         const double m = u[r] * h;
         const double sq4 = m * __builtin_fma(-m, h, 3.0);

@@ -896,7 +896,7 @@ __global__ __launch_bounds__(kBlock) void var_chain_kernel(const VarChainP<T> p)
                 const long long qs = ops[k].qstore;
                 if (qs >= 0 && g < p.n1) {
                     T* q = p.out + n * p.store_total + p.n1 * qs + g * howo;
-                    for (int e = tid; e < howo; e += kBlock) q[e] = T(0.25) * dst[e];
+                    for (int e = tid; e < howo; e += kBlock) q[e] = T(kXVarScale) * dst[e];
                 }
                 lds_barrier();   // a later op may reuse the slot
             }
@@ -1401,6 +1401,8 @@ int chol_blocked(BlasDev* b, hipStream_t s, double* a, int64_t n, int64_t lda, i
 extern "C" {
 
 int cgp_abi_version(void) { return CGP_ABI_VERSION; }
+
+double cgp_net_xvar_scale(void) { return kXVarScale; }
 const char* cgp_last_error(void) { return g_last_error.c_str(); }
 size_t cgp_conv_args_size(void) { return sizeof(cgp_conv_args); }
 size_t cgp_relu_args_size(void) { return sizeof(cgp_relu_args); }

@@ -56,6 +56,10 @@ extern "C" {
 #define CGP_FLAG_GENERIC_CONV 2  /* force the generic conv kernel (tests / A-B timing) */
 
 int cgp_abi_version(void);
+/* The factor cgp_net_f64's closed-form ReLU expects on its x-side variance maps (var_x /
+ * var2_x without CGP_FLAG_EXACT_RELU): 1/16 from ABI 9 (1/4 in ABI 6-8).  cgp_var_chain_*
+ * writes its qstore copies with it; a host scaling maps itself uses this value. */
+double cgp_net_xvar_scale(void);
 const char* cgp_last_error(void);
 /* sizeof of the argument structs, so an FFI can verify its mirror of the layout */
 size_t cgp_conv_args_size(void);
@@ -296,7 +300,8 @@ typedef struct cgp_net_op {
                               map sizes). */
     double weight, bias;   /* CONV: w·Σ + b;  LINEAR: dst = weight·src + bias·add */
     const void* var_x;     /* ReLU input variances of the x images, [n1][h·w]; for
-                              cgp_net_f64 without CGP_FLAG_EXACT_RELU: QUARTERED (v/4, the
+                              cgp_net_f64 without CGP_FLAG_EXACT_RELU: SCALED by
+                              cgp_net_xvar_scale() (v/16 from ABI 9, v/4 before; the
                               scaled closed form; var2_x likewise) */
     const void* var_y;     /* ... of the y images, [n2][h·w] */
     const void* var2_x;    /* dst2's ReLU: variances of the result, [n1][h·w] */
@@ -341,8 +346,8 @@ typedef struct cgp_net_args {
  *   CGP_VAR_HALF     dst = src / 2
  *   CGP_VAR_SUM      dst = c0·t0 (+ c_k·t_k, k = 1..3, left to right; term slot -1 ends)
  * A value is stored when store >= 0: image g's map at out[n·store + g·ho·wo] (n = n1 + n2
- * images, the x images first), and, for g < n1, 0.25 × the map at
- * out[n·store_total + n1·qstore + g·ho·wo] when qstore >= 0 (the quartered x-side maps of
+ * images, the x images first), and, for g < n1, cgp_net_xvar_scale() × the map at
+ * out[n·store_total + n1·qstore + g·ho·wo] when qstore >= 0 (the scaled x-side maps of
  * cgp_net_f64; store_total = Σ of every stored value's ho·wo).  Slots are LDS element
  * offsets, maps row-major [ho][wo].
  */
@@ -357,7 +362,7 @@ typedef struct cgp_var_op {
     int32_t h, w, ho, wo;  /* input and output map sizes */
     int32_t taps, offset, stride, dilation;   /* CONV, as cgp_conv_args */
     int64_t store;         /* per-image element offset of the stored map, -1: not stored */
-    int64_t qstore;        /* ... of its quartered x-side copy, -1: none */
+    int64_t qstore;        /* ... of its scaled x-side copy, -1: none */
     double weight, bias;   /* CONV */
     double coef[4];        /* SUM */
 } cgp_var_op;

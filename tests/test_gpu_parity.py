@@ -821,7 +821,7 @@ def test_var_chain_matches_layer_pipeline(cfg, dt, same):
     if same:
         assert all(var[v][1].data_ptr() == var[v][0].data_ptr() for v in var)
     for v, q in qvar.items():
-        assert torch.equal(q, var[v][0] * 0.25)
+        assert torch.equal(q, var[v][0] * N.load().cgp_net_xvar_scale())
 
 
 def test_var_chain_rejects_maps_grown_by_padding():
