@@ -163,15 +163,14 @@ __device__ __forceinline__ float fma_t(float a, float b, float c) {
 // v_fma_f64 with an SGPR-pair operand and the table lives in SGPRs only while in use.
 // P̃(x4) = P(x4/4)/16: coefficient k scaled by 1/(16·4^k), exact powers of two, so Horner in
 // x4 = 4x rounds exactly like Horner in x (relu_q_n)
-// x-side variance maps the fp64 closed form reads: v / 2^CGP_XVAR_SHIFT (exact).  4 (1/16,
-// ABI 9): its Newton step then yields y = 8/sqrt(t), so u = 4x = 2 - |c/4|·y is one fma with
-// source modifiers, sqrt(t)/2 comes out of the same step and the polynomial's coefficients
-// carry the factor 2 back (exact); 2 (1/4, rounds 2-3) needs a multiply and a min for u
-#ifndef CGP_XVAR_SHIFT
-#define CGP_XVAR_SHIFT 4
-#endif
-constexpr double kXVarScale = CGP_XVAR_SHIFT == 4 ? 0.0625 : 0.25;
-constexpr double kPolyQ = CGP_XVAR_SHIFT == 4 ? 0.125 : 0.0625;   // P̃ = P(x4/4)·kPolyQ
+// x-side variance maps the fp64 closed form reads: v/16 (exact; ABI 9, cgp_net_xvar_scale).
+// Its Newton step then yields y = 8/sqrt(t), so u = 4x = 2 - |c/4|·y is one fma with source
+// modifiers, sqrt(t)/2 comes out of the same step and the polynomial's coefficients carry
+// the factor 2 back (exact).  Rounds 2-3 read v/4 and needed a multiply and a min for u:
+// one op more per pixel, measured 0.9-1.4% slower on all three configs
+// (profiles/r4/ab_r4m_xvar_scale.log)
+constexpr double kXVarScale = 0.0625;
+constexpr double kPolyQ = 0.125;   // P̃(x4) = P(x4/4)·kPolyQ·4^-k per coefficient
 constexpr double poly_q(int k) {
     double v = kReluPolyD[k] * kPolyQ;
     for (int n = 0; n < k; ++n) v *= 0.25;
@@ -302,12 +301,13 @@ __device__ __forceinline__ void relu_fast_n(double (&c)[R], const double (&v1)[R
 // costs 4 ops.  A refinement y = y0(1 + e/2), e = 1 - A·y0², of y0 ≈ rsq(A) is
 // y = r·(3 − m·r) with r = rsq(4A) ≈ y0/2 and m = 4A·r — and 4A·r·(3 − m·r) = 4·sqrt(A).
 // Inputs, all exact scalings of relu_fast's:
-//   v1q = v1/4 (the x-side variance map, quartered by the host; netplan.py),
-//   cq  = c/4  (QIN: the producing conv already applied w/4 and b/4; else one multiply),
-// then T = v1q·v2 + tiny/4 = t/4 gives r = rsq(T) ≈ 2/sqrt(t): Y = r·(3 − T·r·r) = 4/sqrt(t),
-// sqrt(t) = T·r·(3 − T·r·r), and |cq|·Y = |c|/sqrt(t) = |rho|.  With x4 = 4x = 2 − 2|rho|,
+//   v1q = v1/16 (the x-side variance map, scaled by the host: cgp_net_xvar_scale),
+//   cq  = c/4   (QIN: the producing conv already applied w/4 and b/4; else one multiply),
+// then T = v1q·v2 + tiny/16 = t/16 gives r = rsq(T) ≈ 4/sqrt(t): Y = r·(3 − T·r·r) =
+// 8/sqrt(t), T·r·(3 − T·r·r) = sqrt(t)/2, and x4 = 4x = 2 − 2|rho| = 2 − |cq|·Y in one fma
+// (round 3 read v/4, got Y = 4/sqrt(t) and spent a multiply and a min on |rho|).  With
 // 4·sqrt(x) = x4·h·(3 − x4·h·h), h = rsq(x4), the polynomial term is
-// sqrt(t)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/16 at x4/4, and max(c, 0)/2 = cq + |cq|.
+// (sqrt(t)/2)·x4·(4 sqrt x)·P̃(x4) with P̃ = P/8 at x4/4, and max(c, 0)/2 = cq + |cq|.
 // R interleaved Horner chains of degree D with SGPR coefficients t[0..D]
 template <int R, int D>
 __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], ConstD t) {
@@ -338,18 +338,13 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         const double r0 = __builtin_amdgcn_rsq(T);
         const double m = T * r0;
         const double k = __builtin_fma(-m, r0, 3.0);
-        y[r] = r0 * k;      // 4/sqrt(t) (shift 2) or 8/sqrt(t) (shift 4)
-        st[r] = m * k;      // sqrt(t) or sqrt(t)/2
+        y[r] = r0 * k;      // 8/sqrt(t)
+        st[r] = m * k;      // sqrt(t)/2
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if constexpr (CGP_XVAR_SHIFT == 4) {
-            // u = 2 - 2|rho| in one rounding, floored at 2^-51 (|rho| <= 1 - 2^-52 as below)
-            u[r] = __builtin_fmax(__builtin_fma(-__builtin_fabs(c[r]), y[r], 2.0), 2.0 - 2.0 * kRhoMax);
-        } else {
-            const double a = __builtin_fmin(__builtin_fabs(c[r] * y[r]), kRhoMax);
-            u[r] = __builtin_fma(-2.0, a, 2.0);
-        }
+        // u = 2 - 2|rho| in one rounding, floored at 2^-51 (|rho| <= 1 - 2^-52, above)
+        u[r] = __builtin_fmax(__builtin_fma(-__builtin_fabs(c[r]), y[r], 2.0), 2.0 - 2.0 * kRhoMax);
         const double h = __builtin_amdgcn_rsq(u[r]);
         const double m = u[r] * h;
         const double sq4 = m * __builtin_fma(-m, h, 3.0);
