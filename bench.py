@@ -60,6 +60,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 import traceback
 
@@ -82,17 +83,7 @@ CLOCK_HZ = 2.4e9               # peak engine clock
 # the older one)
 PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r4", "r3")]
 CALIB_FILES = [os.path.join(ROOT, "profiles", r, "cpu_calibration.json") for r in ("r4", "r2")]
-DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "300"))
-PIPELINE_NOTE = (
-    "cnn_gp.pipeline.classify_distributed: Kxx row strips (B=4096 tiles) balanced by "
-    "evaluated pairs, received point-to-point into the full matrix on rank 0 (RCCL with "
-    "nccl; that path first runs on the driver's multi-GPU node: every multi-rank run so "
-    "far used gloo ranks sharing one GPU); rank 0 factors it (blocked dpotrf/dtrsm/dsyrk, "
-    "nb 2048) while the other ranks build their Kxz row strips (rank 0's share sized to "
-    "end with them); alpha broadcast, scores = Kxz rows @ alpha per rank, only the scores "
-    "gathered; solver code objects loaded on a side thread during the Kxx build; spot "
-    "check = HIP vs HIP single pairs in the computed orientation (oracle parity at this "
-    "geometry: tests/test_gpu_fullgeom.py, tests/test_gpu_fullscale_bound.py)")
+DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "120"))
 
 
 def parse(argv=None):
@@ -111,6 +102,9 @@ def parse(argv=None):
     p.add_argument("--no-cifar10", action="store_true", help="skip the cifar10 Kxx leg")
     p.add_argument("--no-f32", action="store_true",
                    help="skip the float32 repeat of the Kxx legs")
+    p.add_argument("--no-dropin", action="store_true",
+                   help="skip the literal save_kernel.py loop (save_K + per-tile kern)")
+    p.add_argument("--dropin-n", type=int, default=2048)
     p.add_argument("--no-fullscale", action="store_true")
     p.add_argument("--no-fullscale-f32", action="store_true",
                    help="skip the float32-kernel repeat of the full-scale leg")
@@ -179,6 +173,65 @@ def launch_or_check(args, argv):
 # legs: one failure costs its own slot, not the line
 # ------------------------------------------------------------------------------------------
 
+class Deadline:
+    """The run's wall-clock budget (the driver allows the bench 600 s).  A leg that would
+    start after ``budget_s`` (its estimate included) is recorded as skipped; at ``hard_s``
+    a watchdog on rank 0 prints the line from what has been recorded and ends the process
+    (a hung collective cannot hold the line back).  CGP_BENCH_BUDGET_S / CGP_BENCH_HARD_S
+    override the defaults (420 s / 540 s)."""
+
+    def __init__(self, budget_s=None, hard_s=None, t0=None):
+        env = os.environ.get
+        self.budget_s = float(budget_s if budget_s is not None
+                              else env("CGP_BENCH_BUDGET_S", "420"))
+        self.hard_s = float(hard_s if hard_s is not None else env("CGP_BENCH_HARD_S", "540"))
+        self.t0 = time.monotonic() if t0 is None else t0
+
+    def elapsed(self):
+        return time.monotonic() - self.t0
+
+    def over(self, est_s=0.0):
+        return self.elapsed() + est_s > self.budget_s
+
+
+class Emitter:
+    """Prints the one JSON line exactly once: from the main thread at the end of the run,
+    or from the watchdog at the hard deadline, whichever comes first."""
+
+    def __init__(self, write=None):
+        self.lock = threading.Lock()
+        self.done = False
+        self.write = write or (lambda s: (sys.stdout.write(s + "\n"), sys.stdout.flush()))
+
+    def emit(self, make_line) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            self.write(json.dumps(make_line()))
+            return True
+
+
+class Watchdog(threading.Thread):
+    """Rank 0's guard against a leg that never returns (e.g. a collective whose peer hung):
+    at the deadline's hard limit it emits the line (the running leg marked) and calls
+    ``exit_fn`` (default os._exit(3): torchrun then tears the other ranks down)."""
+
+    def __init__(self, deadline, emitter, make_line, exit_fn=None):
+        super().__init__(daemon=True, name="bench-watchdog")
+        self.deadline, self.emitter, self.make_line = deadline, emitter, make_line
+        self.exit_fn = exit_fn or (lambda: os._exit(3))
+        self.stop = threading.Event()
+
+    def run(self):
+        if self.stop.wait(max(0.0, self.deadline.hard_s - self.deadline.elapsed())):
+            return
+        print(f"bench.py: watchdog: {self.deadline.hard_s:.0f} s reached, printing the line",
+              file=sys.stderr, flush=True)
+        if self.emitter.emit(lambda: self.make_line(watchdog=True)):
+            self.exit_fn()
+
+
 class Legs:
     """Runs each measurement leg and agrees on its outcome across the ranks.
 
@@ -186,23 +239,42 @@ class Legs:
     ranks every rank's outcome is exchanged over a gloo side group (``group``: host
     memory, its own timeout, independent of the RCCL communicator's state), and once any
     rank has failed a leg the remaining multi-rank legs are skipped — a collective could
-    otherwise pair with a different leg's on another rank.  CGP_BENCH_FAIL_LEG=<name>[,…]
-    forces a failure (tests of this mechanism)."""
+    otherwise pair with a different leg's on another rank.  A leg that would start past
+    the deadline's budget (``est_s`` its expected duration) is skipped on every rank (the
+    ranks agree on it first).  CGP_BENCH_FAIL_LEG=<name>[,…] forces a failure and
+    CGP_BENCH_HANG_LEG=<name>:<rank> makes that rank block inside the leg (tests of these
+    mechanisms)."""
 
-    def __init__(self, world: int = 1, rank: int = 0, group=None):
+    def __init__(self, world: int = 1, rank: int = 0, group=None, deadline=None):
         self.world, self.rank, self.group = world, rank, group
+        self.deadline = deadline
         self.stopped = None
+        self.current = None
 
-    def run(self, name, fn, multi_rank=True):
+    def _agree(self, flag):
+        flags = [None] * self.world
+        dist.all_gather_object(flags, flag, group=self.group)
+        return any(flags)
+
+    def run(self, name, fn, multi_rank=True, est_s=0.0):
         if self.stopped and multi_rank and self.world > 1:
             return {"error": f"skipped: leg {self.stopped!r} failed on a rank"}
+        over = self.deadline is not None and self.deadline.over(est_s)
+        if self.world > 1 and multi_rank:
+            over = self._agree(over)
+        if over:
+            return {"error": f"skipped: budget ({self.deadline.elapsed():.0f} s used, "
+                             f"~{est_s:.0f} s needed, {self.deadline.budget_s:.0f} s allowed)"}
         err, out = None, None
+        self.current = name
         try:
             if name in os.environ.get("CGP_BENCH_FAIL_LEG", "").split(","):
                 raise RuntimeError(f"forced failure of leg {name!r} (CGP_BENCH_FAIL_LEG)")
+            if f"{name}:{self.rank}" in os.environ.get("CGP_BENCH_HANG_LEG", "").split(","):
+                threading.Event().wait()          # blocks for good (watchdog test)
             out = fn()
         except Exception as e:                 # noqa: BLE001 — recorded, never swallowed
-            err = f"{type(e).__name__}: {e}"[:1000]
+            err = f"{type(e).__name__}: {e}"[:300]
             print(f"bench.py: rank {self.rank}: leg {name!r} failed", file=sys.stderr)
             traceback.print_exc(file=sys.stderr)
             out = None
@@ -213,13 +285,16 @@ class Legs:
             try:
                 dist.all_gather_object(errs, err, group=self.group)
             except Exception as e:             # noqa: BLE001
-                errs = [f"leg status exchange failed: {type(e).__name__}: {e}"]
+                errs = [f"leg status exchange failed: {type(e).__name__}: {e}"[:300]]
             bad = {str(r): m for r, m in enumerate(errs) if m}
+            self.current = None
             if bad:
                 self.stopped = name
                 return {"error": bad}
         elif err:
+            self.current = None
             return {"error": err}
+        self.current = None
         return out
 
 
@@ -548,18 +623,7 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     mk = model_kern(model)
 
     def step():
-        # one Gram build: every image's variance maps once (ModelKern.bind), then each
-        # tile from slices of them, written in place into K (cnn_gp.gram's builders)
-        bound = mk.bind(X)
-        with torch.no_grad():
-            for same, i, j in tiles:
-                a, b = min(B, n_total - i * B), min(B, n_total - j * B)
-                view = K[i * B:i * B + a, j * B:j * B + b]
-                if bound is not None:
-                    bound.tile((same, i * B, j * B, a, b), view)
-                    continue
-                xi = X[i * B:(i + 1) * B]
-                view.copy_(model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False))
+        build_kxx(mk, model, X, K, tiles, B, n_total)
 
     for _ in range(warmup):
         step()
@@ -623,12 +687,233 @@ def kxx_leg(cfg_name, args, B, world, rank, dev, dtype, backend, probe, group, s
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# the drop-in path itself: save_kernel.py's loop, timed
+# ------------------------------------------------------------------------------------------
+
+class MemH5:
+    """In-memory stand-in for the h5py.File save_K writes (h5py is not installed here):
+    create_dataset(...) -> a NaN-filled float32 numpy array with slice assignment."""
+
+    def __init__(self):
+        self.d = {}
+
+    def keys(self):
+        return self.d.keys()
+
+    def create_dataset(self, name, shape, dtype, fillvalue, chunks, maxshape):
+        import numpy as np
+        self.d[name] = np.full(shape, fillvalue, dtype=dtype)
+        return self.d[name]
+
+
+def build_kxx(mk, model, X, K, tiles, B, n):
+    """One Gram build of the bench's step: every image's variance maps once
+    (ModelKern.bind), then each tile written in place into K (cnn_gp.gram's builders)."""
+    bound = mk.bind(X)
+    with torch.no_grad():
+        for same, i, j in tiles:
+            a, b = min(B, n - i * B), min(B, n - j * B)
+            view = K[i * B:i * B + a, j * B:j * B + b]
+            if bound is not None:
+                bound.tile((same, i * B, j * B, a, b), view)
+                continue
+            xi = X[i * B:(i + 1) * B]
+            view.copy_(model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False))
+
+
+def dropin_leg(cfg_names, n, tiles, dev):
+    """exp_mnist_resnet/save_kernel.py:19-29 verbatim in effect: the float32 model
+    (config.initial_model.cuda()), host float32 images in a Dataset, and
+    ``kern(x, x2, same, diag) = model(x.cuda(), x2.cuda(), same, diag).cpu().numpy()`` driven
+    tile by tile by save_K (kernel_save_tools.py:26-58: ProductIterator batches, the
+    isfinite check, the write into a float32 (1, N, N) dataset; an in-memory stand-in for
+    the h5py file).  Beside it, the bound build (the bench's step: maps once, tiles in
+    place, no host copies) on the same images, model and tile size; the two matrices are
+    compared on the upper tiles.  pairs = N(N−1)/2 for both (the headline's count)."""
+    import contextlib
+    import numpy as np
+    from torch.utils.data import Subset, TensorDataset
+    from cnn_gp.kernel_save_tools import save_K
+    pairs = n * (n - 1) // 2
+    out = {}
+    for name in cfg_names:
+        cfg = importlib.import_module(f"configs.{name}")
+        model = cfg.initial_model.to(dev)           # float32 buffers: save_kernel.py:19
+        C = getattr(cfg, "in_channels", 1)
+        side = 32 if C == 3 else 28
+        g = torch.Generator().manual_seed(0)
+        X = torch.rand((n, C, side, side), generator=g, dtype=torch.float32)
+        ds = TensorDataset(X, torch.zeros(n, dtype=torch.int64))
+
+        def kern(x, x2, same, diag):                # save_kernel.py:21-24
+            with torch.no_grad():
+                return model(x.cuda(dev), x2.cuda(dev), same, diag).detach().cpu().numpy()
+
+        Xd = X.to(dev)
+        mk = model_kern(model)
+        for B in tiles:
+            with contextlib.redirect_stdout(sys.stderr):   # save_K's progress lines
+                save_K(MemH5(), kern, "Kxx", Subset(ds, range(min(n, 2 * B))), None, False, B)
+                torch.cuda.synchronize()
+                f = MemH5()
+                t0 = time.perf_counter()
+                save_K(f, kern, "Kxx", ds, None, False, B, print_interval=1e9)
+                el = time.perf_counter() - t0
+            K = torch.full((n, n), float("nan"), dtype=torch.float32, device=dev)
+            sched = tile_schedule(n, None, B, 0, 1)
+            build_kxx(mk, model, Xd, K, sched, B, n)        # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            build_kxx(mk, model, Xd, K, sched, B, n)
+            torch.cuda.synchronize()
+            el_b = time.perf_counter() - t0
+            Kf, Kb = f.d["Kxx"][0], K.cpu().numpy()
+            mask = ~np.isnan(Kf)
+            diff = float(np.max(np.abs(Kf[mask] - Kb[mask]) / np.abs(Kb[mask])))
+            del K
+            out[f"{name}/B{B}"] = {
+                "pairs_per_s": round(pairs / el), "s": round(el, 4), "tiles": len(sched),
+                "ms_per_tile": round(el / len(sched) * 1e3, 3),
+                "bound_pairs_per_s": round(pairs / el_b), "over_bound": round(el_b / el, 3),
+                "max_rel_diff_vs_bound": diff}
+        del Xd
+        torch.cuda.empty_cache()
+    return {"n": n, "dtype": "f32", "cases": out}
+
+
+# ------------------------------------------------------------------------------------------
+# the line: every leg's numbers, compact (the driver keeps ~8 KB of stdout)
+# ------------------------------------------------------------------------------------------
+
+LINE_MAX_CHARS = 7000
+
+
+def _sig(x, digits=4):
+    """x rounded to ``digits`` significant digits (ints and None pass through)"""
+    if not isinstance(x, float) or x != x or x in (float("inf"), float("-inf")):
+        return x
+    if x == 0.0:
+        return 0.0
+    import math
+    d = digits - int(math.floor(math.log10(abs(x)))) - 1
+    return round(x, d) if d > 0 else float(round(x, d))
+
+
+def _pick(d, keys, digits=4):
+    if not isinstance(d, dict):
+        return d
+    if "error" in d:
+        e = d["error"]
+        return {"error": e if isinstance(e, str) else {k: str(v)[:200] for k, v in e.items()}}
+    return {k: _sig(d[k], digits) for k in keys if d.get(k) is not None}
+
+
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "avg_ms",
+              "valu_issue_frac", "valu_insts_per_pair", "launches")
+_CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "reference_equivalent_pairs_per_s")
+_FS_KEYS = ("n", "m", "total_s", "kxx_s", "kxx_pairs_per_s", "kxz_s", "kxz_s_rank0",
+            "gather_kxx_s", "solve_s", "solve_tflops", "predict_s", "residual",
+            "spot_check_hip_vs_hip_max_rel_err", "spot_vs_f64_max_rel_err",
+            "rank0_peak_gather_solve_over_kxx", "fullscale_wall_s")
+
+
+def _cpu(c):
+    if not isinstance(c, dict) or "error" in c:
+        return _pick(c, ())
+    out = _pick(c, _CPU_KEYS)
+    out["sample"] = str(c.get("sample", ""))[:90]
+    return out
+
+
+def _kxx_leg(d):
+    if not isinstance(d, dict) or "error" in d:
+        return _pick(d, ())
+    out = {"value": round(d["value"]), "ms_per_step": _sig(d["ms_per_step"]),
+           "workload": d["config"]["workload"], "roofline": _pick(d.get("roofline"), _ROOF_KEYS)}
+    if d.get("cpu_baseline") is not None:
+        out["cpu_baseline"] = _cpu(d["cpu_baseline"])
+    if len(d.get("ranks") or []) > 1:
+        out["ranks_ms"] = [_sig(r["ms_per_step"]) for r in d["ranks"]]
+    return out
+
+
+def _fullscale(d):
+    if not isinstance(d, dict) or "error" in d:
+        return _pick(d, ())
+    out = _pick(d, _FS_KEYS, 5)
+    sp = d.get("solve_split") or {}
+    out.update({k: _sig(sp[k]) for k in ("factor_s", "factor_tflops", "potrs_s", "widen_s")
+                if sp.get(k) is not None})
+    if d.get("harness_s") is not None:
+        out["residual_rows_s_outside_solve"] = _sig(d["harness_s"])
+    if d.get("ranks"):
+        out["ranks"] = {k: [_sig(r.get(k)) for r in d["ranks"]]
+                        for k in ("kxx_s", "gather_kxx_s", "kxz_s")}
+    return out
+
+
+def compact_line(full: dict) -> dict:
+    """The printed line: the headline keys of the bench contract, then every leg with its
+    value, roofline and CPU baseline, headline-first and full-scale last; per-leg prose,
+    plans and per-rank dicts stay in the full result file (``full_result``) and in
+    DESIGN.md §6.  Kept under LINE_MAX_CHARS (tests/test_bench_launcher.py)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+    line = {k: full.get(k) for k in keep}
+    line["value"] = None if full.get("value") is None else round(full["value"])
+    cfg = full.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "n", "tile", "pairs_per_step",
+                                          "parallelism") if k in cfg}
+    if full.get("world", 1) > 1:
+        line["backend"] = full.get("backend")
+        line["ranks_ms"] = [_sig(r["ms_per_step"]) for r in (full.get("ranks") or [])
+                            if isinstance(r, dict) and "ms_per_step" in r]
+    for k in ("error", "watchdog"):
+        if full.get(k) is not None:
+            line[k] = str(full[k])[:300]
+    line["roofline"] = _pick(full.get("roofline"), _ROOF_KEYS)
+    line["cpu_baseline"] = _cpu(full.get("cpu_baseline"))
+    line["reference_schedule_pairs_per_s"] = _sig(full.get("reference_schedule_pairs_per_s"))
+    if "conv_stencil_roofline" in full:
+        line["conv_stencil_roofline"] = _pick(
+            full["conv_stencil_roofline"], ("bound", "achieved", "peak", "unit", "frac",
+                                            "traffic", "kernel", "avg_ms", "pmc_avg_ms",
+                                            "alg_bytes_per_launch", "torch_copy_GBs"))
+    for k in ("mnist_as_tf", "cifar10"):
+        if k in full:
+            line[k] = _kxx_leg(full[k])
+    if "solve" in full:
+        line["solve"] = _pick(full["solve"], ("n", "s", "factor_s", "factor_tflops", "potrs_s",
+                                              "build_solve_wall_s"))
+    if "dropin" in full:
+        d = full["dropin"]
+        if isinstance(d, dict) and "cases" in d:
+            line["dropin"] = {"n": d["n"], "dtype": d["dtype"], **{
+                k: _pick(v, ("pairs_per_s", "ms_per_tile", "bound_pairs_per_s", "over_bound",
+                             "max_rel_diff_vs_bound"), 3) for k, v in d["cases"].items()}}
+        else:
+            line["dropin"] = _pick(d, ())
+    if "f32" in full:
+        f = full["f32"]
+        line["f32"] = {k: round(v["value"]) for k, v in f.items() if isinstance(v, dict)
+                       and "value" in v} if "error" not in f else _pick(f, ())
+    for k in ("fullscale", "fullscale_f32", "fullscale_cifar10"):
+        if k in full:
+            line[k] = _fullscale(full[k])
+    if full.get("full_result"):
+        line["full_result"] = full["full_result"]
+    line["notes"] = "per-leg definitions: DESIGN.md §6; full result: full_result"
+    return line
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     rc = launch_or_check(args, argv)
     if rc is not None:
         return rc
+    deadline = Deadline()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -649,28 +934,85 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
             dist.init_process_group(backend, timeout=tmo)
+        # the status exchange waits for a rank still inside a timed-out collective; the
+        # watchdog bounds the whole run
         status = dist.new_group(backend="gloo",
-                                timeout=datetime.timedelta(seconds=2 * DIST_TIMEOUT_S + 60))
-    legs = Legs(world, rank, status)
+                                timeout=datetime.timedelta(seconds=DIST_TIMEOUT_S + 60))
+    legs = Legs(world, rank, status, deadline)
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
     B = args.tile
     probe = not args.no_probe
-    extra = {}
+    full = {
+        "metric": "kernel entries/s (N×M pairs) + full-Kxx build+solve wall-clock, "
+                  "MNIST 28×28",
+        "value": None, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (torch.rand seed 0, 28x28x1)",
+        "config": {"workload": f"{args.config} Kxx {args.n}x{args.n}, tiles {B}",
+                   "n": args.n, "tile": B, "parallelism": f"tiles-dp{world}"},
+        "world": world, "backend": backend if world > 1 else None,
+        "value_counts": "pairs the device evaluates: i < j on diagonal tiles",
+        "roofline": None, "cpu_baseline": None}
+    full_path = os.environ.get("CGP_BENCH_FULL_OUT",
+                               os.path.join(ROOT, "gpurun_out", "bench_full.json"))
+    full["full_result"] = os.path.relpath(full_path, ROOT)
+
+    def make_line(watchdog=False):
+        snap = dict(full)
+        if watchdog:
+            snap["watchdog"] = (f"hard limit {deadline.hard_s:.0f} s reached during leg "
+                                f"{legs.current!r}; later legs not run")
+        return compact_line(snap)
+
+    emitter = Emitter()
+    dog = None
+    if rank == 0:
+        dog = Watchdog(deadline, emitter, make_line)
+        dog.start()
 
     def put(name, value):
         if rank == 0 and value is not None:
-            extra[name] = value
+            full[name] = value
 
     # --- the headline: BASELINE configs[1] ---
     r = legs.run("headline", lambda: time_config(args.config, args.n, B, args.steps,
                                                  args.warmup, world, rank, dev, dtype,
                                                  backend, probe))
     failed = "error" in r
-    ranks = None
-    if not failed:
-        ranks = legs.run("rank_stats", lambda: gather_rank_stats(r["rank_stats"], world,
-                                                                   status))
-    n_total = None if failed else r["n_total"]
+    if failed:
+        full["error"] = r["error"]
+    else:
+        n_total = r["n_total"]
+        full.update(value=r["value"], ms_per_step=round(r["ms_step"], 3),
+                    reference_schedule_pairs_per_s=round(r["ref_sched_value"], 1),
+                    unique_entries_per_s=round(r["unique"], 1))
+        full["config"].update(workload=f"{args.config} Kxx {n_total}x{n_total}, tiles {B}",
+                              n=n_total, tiles_total=len(r["all_tiles"]),
+                              tiles_rank0=len(r["tiles"]), pairs_per_step=r["evaluated"])
+        full["ranks"] = legs.run("rank_stats", lambda: gather_rank_stats(r["rank_stats"],
+                                                                         world, status))
+
+    # --- dominant kernel (timed live in the headline) and the Conv2d stencil alone ---
+    if not failed and rank == 0 and probe:
+        full["roofline"] = legs.run("roofline", lambda: net_roofline(
+            r["model"], r["X"][:B], args.config, r["timing"]), multi_rank=False)
+
+        def stencil():
+            with torch.no_grad():
+                return conv_stencil_roofline(r["model"], r["X"][:B], B)
+        put("conv_stencil_roofline", legs.run("conv_stencil_roofline", stencil,
+                                              multi_rank=False))
+
+    # --- BASELINE configs[2] (ResNet-GP) on the same harness, with its CPU baseline ---
+    cpu_ok = world == 1 and not args.no_cpu
+    if not args.no_second and args.config != "mnist_as_tf":
+        put("mnist_as_tf", legs.run("mnist_as_tf", lambda: kxx_leg(
+            "mnist_as_tf", args, B, world, rank, dev, dtype, backend, probe, status,
+            max(2, args.steps // 4), cpu_ok), est_s=40))
+    if rank == 0 and cpu_ok:
+        full["cpu_baseline"] = legs.run("cpu_baseline", lambda: cpu_baseline(
+            args.config, dtype, args.cpu_seconds), multi_rank=False, est_s=20)
 
     # --- solve of the assembled Kxx (single GPU) ---
     def solve_leg():
@@ -696,39 +1038,25 @@ def main(argv=None):
                 "factor_tflops": round(n_total ** 3 / 3 / max(ph["factor_s"], 1e-9) / 1e12, 3),
                 "peak_tflops": FP64_PEAK_TFLOPS, **ph,
                 "copy_and_transposes_s": round(t_solve - sum(ph.values()), 5),
-                "build_solve_wall_s": round(r["ms_step"] / 1e3 + t_solve, 4),
-                "note": "blocked dpotrf/dtrsm/dsyrk + dpotrs_64 (10 rhs) on a device copy "
-                        "of Kxx (NaN lower triangle), best of 3 after a warm-up; phases "
-                        "from HIP events inside cgp_chol_solve_f64"}
+                "build_solve_wall_s": round(r["ms_step"] / 1e3 + t_solve, 4)}
 
     if not failed and rank == 0 and world == 1 and not args.no_solve:
-        put("solve", legs.run("solve", solve_leg, multi_rank=False))
-
-    # --- dominant kernel, timed live ---
-    roof = None
-    if not failed and rank == 0 and probe:
-        roof = legs.run("roofline", lambda: net_roofline(r["model"], r["X"][:B], args.config,
-                                                         r["timing"]), multi_rank=False)
-
-        def stencil():
-            with torch.no_grad():
-                return conv_stencil_roofline(r["model"], r["X"][:B], B)
-        put("conv_stencil_roofline", legs.run("conv_stencil_roofline", stencil,
-                                              multi_rank=False))
+        put("solve", legs.run("solve", solve_leg, multi_rank=False, est_s=5))
     if not failed:
         del r["K"]
     torch.cuda.empty_cache()
 
-    # --- BASELINE configs[2] (ResNet-GP) and configs[4]'s network on the same harness ---
-    cpu_ok = world == 1 and not args.no_cpu
-    if not args.no_second and args.config != "mnist_as_tf":
-        put("mnist_as_tf", legs.run("mnist_as_tf", lambda: kxx_leg(
-            "mnist_as_tf", args, B, world, rank, dev, dtype, backend, probe, status,
-            max(2, args.steps // 4), cpu_ok)))
+    # --- configs[4]'s network on the same harness ---
     if not args.no_cifar10 and args.config != "cifar10":
         put("cifar10", legs.run("cifar10", lambda: kxx_leg(
             "cifar10", args, B, world, rank, dev, dtype, backend, probe, status,
-            max(2, args.steps // 4), cpu_ok)))
+            max(2, args.steps // 4), cpu_ok), est_s=40))
+
+    # --- the literal drop-in path (save_kernel.py's loop), beside the bound build ---
+    if rank == 0 and not args.no_dropin:
+        put("dropin", legs.run("dropin", lambda: dropin_leg(
+            (args.config, "mnist_as_tf"), args.dropin_n, (200, 1024), dev),
+            multi_rank=False, est_s=20))
 
     # --- the same workloads at the reference pipeline's own kernel precision ---
     # (exp_mnist_resnet/save_kernel.py runs the float32 model; kernel_save_tools.py:21
@@ -745,15 +1073,11 @@ def main(argv=None):
                              "ms_per_step": round(r3["ms_step"], 3),
                              "pairs_per_step": r3["evaluated"]}
                 torch.cuda.empty_cache()
-            f32["note"] = ("float32 model and images, as the reference's save_kernel.py runs "
-                           "them; same Kxx harness as the fp64 legs.  Entries stay within "
-                           "3e-7 relative of the fp64 kernel (tests/test_gpu_parity.py "
-                           "test_f32_kernel_within_north_star_tolerance; north star 1e-5)")
             return f32 if rank == 0 else None
-        put("f32", legs.run("f32", f32_leg))
+        put("f32", legs.run("f32", f32_leg, est_s=20))
 
     # --- BASELINE configs[3] / [4]: the full-scale ResNet-GP pipelines ---
-    def fullscale_leg(config, n, kernel_dtype, data, note):
+    def fullscale_leg(config, n, kernel_dtype, data):
         from fullscale import fullscale
         t0 = time.perf_counter()
         fs = fullscale(config, n, args.fullscale_m, 4096, rank=rank, world=world, dev=dev,
@@ -762,68 +1086,37 @@ def main(argv=None):
             return None
         fs["fullscale_wall_s"] = round(time.perf_counter() - t0, 2)
         fs["data"] = data
-        fs["note"] = note
         return fs
 
+    # expected durations at one GPU, shrinking with the ranks (strong scaling)
+    def est(s1):
+        return s1 / world + 15
     mnist_data = "synthetic MNIST-like (k/255, 60% zeros, 4-px zero border)"
     if not args.no_fullscale and dtype == torch.float64:
         put("fullscale", legs.run("fullscale", lambda: fullscale_leg(
-            "mnist_as_tf", args.fullscale_n, torch.float64, mnist_data, PIPELINE_NOTE)))
-        if not args.no_fullscale_f32:
-            # the same pipeline at the reference pipeline's own kernel precision
-            # (save_kernel.py runs the float32 model; K stored float32, widened to float64
-            # for the solve by classify_gp.py's load_kern)
-            put("fullscale_f32", legs.run("fullscale_f32", lambda: fullscale_leg(
-                "mnist_as_tf", args.fullscale_n, torch.float32, mnist_data,
-                "kernels in float32 as exp_mnist_resnet/save_kernel.py runs them; K widened "
-                "to float64 on the device for the rocSOLVER solve; spot_vs_f64_max_rel_err "
-                "= float32 entries against the float64 model (north-star tolerance 1e-5)")))
+            "mnist_as_tf", args.fullscale_n, torch.float64, mnist_data), est_s=est(60)))
     if not args.no_fullscale_cifar10 and dtype == torch.float64:
         put("fullscale_cifar10", legs.run("fullscale_cifar10", lambda: fullscale_leg(
             "cifar10", args.cifar10_n, torch.float64,
-            "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)",
-            "BASELINE configs[4] (configs/cifar10.py:4-47 architecture). " + PIPELINE_NOTE)))
-
-    cpu = None
-    if rank == 0 and cpu_ok:
-        cpu = legs.run("cpu_baseline", lambda: cpu_baseline(args.config, dtype,
-                                                            args.cpu_seconds),
-                       multi_rank=False)
+            "synthetic CIFAR-like 3x32x32 (k/255, 60% zeros, 4-px zero border)"),
+            est_s=est(55)))
+    if not args.no_fullscale and not args.no_fullscale_f32 and dtype == torch.float64:
+        # the same pipeline at the reference pipeline's own kernel precision
+        # (save_kernel.py runs the float32 model; K stored float32, widened to float64
+        # for the solve by classify_gp.py's load_kern)
+        put("fullscale_f32", legs.run("fullscale_f32", lambda: fullscale_leg(
+            "mnist_as_tf", args.fullscale_n, torch.float32, mnist_data), est_s=est(35)))
 
     if rank == 0:
-        line = {
-            "metric": "kernel entries/s (N×M pairs) + full-Kxx build+solve wall-clock, "
-                      "MNIST 28×28",
-            "value": None if failed else round(r["value"], 1),
-            "unit": "pairs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": None if failed else round(r["ms_step"], 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic (torch.rand seed 0, 28x28x1)",
-            "config": {"workload": f"{args.config} Kxx {n_total}x{n_total}, tiles {B}",
-                       "n": n_total, "tile": B,
-                       "tiles_total": None if failed else len(r["all_tiles"]),
-                       "tiles_rank0": None if failed else len(r["tiles"]),
-                       "pairs_per_step": None if failed else r["evaluated"],
-                       "parallelism": f"tiles-dp{world}"},
-            "world": world,
-            "backend": backend if world > 1 else None,
-            "value_counts": "pairs the device evaluates: i < j on diagonal tiles",
-            "reference_schedule_pairs_per_s": None if failed else round(r["ref_sched_value"], 1),
-            "unique_entries_per_s": None if failed else round(r["unique"], 1),
-            "ranks": ranks,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
-        if failed:
-            line["error"] = r["error"]
-        line.update(extra)
-        print(json.dumps(line), flush=True)
+        full["elapsed_s"] = round(deadline.elapsed(), 1)
+        try:
+            os.makedirs(os.path.dirname(full_path), exist_ok=True)
+            with open(full_path, "w") as fh:
+                json.dump(full, fh, default=str)
+        except OSError as e:
+            print(f"bench.py: could not write {full_path}: {e}", file=sys.stderr)
+        dog.stop.set()
+        emitter.emit(make_line)
     if world > 1:
         try:
             dist.destroy_process_group()

@@ -121,7 +121,8 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          solve_tflops: float = SOLVE_TFLOPS,
                          widen: Optional[Callable] = None, log: Optional[Callable] = None,
                          warm: Optional[Callable] = None, cast: Optional[Callable] = None,
-                         rank_times: Optional[dict] = None):
+                         rank_times: Optional[dict] = None,
+                         pre_solve: Optional[Callable] = None):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
 
@@ -140,6 +141,9 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     end of the Kxx build: the gather, the solve and the Kxz phase); None on the other
     ranks.  ``rank_times`` (optional dict) is filled on EVERY rank with that rank's own
     phase times and pairs (kxx_s, gather_kxx_s, kxz_s, predict_s, kxx_pairs, kxz_pairs).
+    ``pre_solve(K)`` (optional) runs on ``dst`` with the assembled matrix just before the
+    solve, outside ``solve_s`` (its time is ``pre_solve_s``): a caller's look at K before a
+    solve that factors it in place (e.g. tools/fullscale.py's residual rows).
 
     Each rank binds only the images its strips read: a Kxx strip [r0, r1) touches rows
     and columns >= r0 (X[r0:]), a Kxz strip [z0, z1) the images Z[z0:z1] against all of
@@ -217,6 +221,11 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     alpha = None
     failure = None
     if rank == dst:
+        if pre_solve is not None:
+            tp = time.perf_counter()
+            pre_solve(K)
+            _sync(dev)
+            res["pre_solve_s"] = round(time.perf_counter() - tp, 4)
         t2 = time.perf_counter()
         if K.dtype == out_dtype:
             Kd = K

@@ -148,3 +148,140 @@ def test_help_lists_every_leg_switch():
     assert p.returncode == 0
     for flag in ("--no-cifar10", "--no-fullscale", "--no-fullscale-cifar10", "--gpus"):
         assert flag in p.stdout
+
+
+def _recorded_full(world=1):
+    """A full result in bench.py's format: profiles/r4/bench_r4s_final_box2.json (a
+    whole round-4 line, every leg) plus the legs added since, at ``world`` ranks."""
+    import copy
+    import json
+    with open(os.path.join(ROOT, "profiles", "r4", "bench_r4s_final_box2.json")) as f:
+        full = json.load(f)
+    full = copy.deepcopy(full)
+    full["world"] = full["n_gpus"] = world
+    case = {"pairs_per_s": 41234567, "s": 0.0508, "tiles": 66, "ms_per_tile": 0.7712,
+            "bound_pairs_per_s": 151234567, "over_bound": 0.2727,
+            "max_rel_diff_vs_bound": 1.234e-7}
+    full["dropin"] = {"n": 2048, "dtype": "f32", "cases": {
+        f"{c}/B{b}": dict(case) for c in ("mnist_paper_convnet_gp", "mnist_as_tf")
+        for b in (200, 1024)}}
+    full["full_result"] = "gpurun_out/bench_full.json"
+    if world > 1:
+        full["backend"] = "nccl"
+        full["ranks"] = [{"rank": r, "tiles": 18, "pairs_per_step": 8386560,
+                          "ms_per_step": 80.123 + r} for r in range(world)]
+        for leg in ("mnist_as_tf", "cifar10"):
+            full[leg]["ranks"] = full["ranks"]
+        for leg in ("fullscale", "fullscale_f32", "fullscale_cifar10"):
+            full[leg]["ranks"] = [{"rank": r, "kxx_s": 5.123456, "kxx_pairs": 224999999,
+                                   "gather_kxx_s": 0.512345, "kxz_s": 1.712345,
+                                   "kxz_pairs": 75000000, "kxz_rows": [0, 1250],
+                                   "kxx_rows": [0, 2048], "predict_s": 0.001}
+                                  for r in range(world)]
+            full[leg]["harness_s"] = 0.1701
+    return full
+
+
+def test_line_fits_the_driver_stdout_tail():
+    """The driver keeps ~8 KB of the bench's stdout: the printed line (compact_line of the
+    full result) stays below 7 000 characters at 1 and 8 ranks and keeps every leg's
+    value, roofline and CPU baseline."""
+    import json
+    b = _bench()
+    for world in (1, 8):
+        full = _recorded_full(world)
+        line = b.compact_line(full)
+        s = json.dumps(line)
+        assert len(s) < b.LINE_MAX_CHARS == 7000, (world, len(s))
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+            assert k in line
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+            assert k in line["roofline"] and k in line["conv_stencil_roofline"]
+            assert k in line["mnist_as_tf"]["roofline"] and k in line["cifar10"]["roofline"]
+        for k in ("value", "unit", "cores", "kind", "sample"):
+            assert k in line["cpu_baseline"] and k in line["mnist_as_tf"]["cpu_baseline"]
+        assert line["conv_stencil_roofline"]["frac"] == full["conv_stencil_roofline"]["frac"]
+        assert line["value"] == round(full["value"])
+        assert len(line["dropin"]) == 2 + 4
+        for leg in ("fullscale", "fullscale_f32", "fullscale_cifar10"):
+            assert line[leg]["total_s"] == full[leg]["total_s"]
+        if world > 1:
+            assert len(line["ranks_ms"]) == world
+            assert len(line["fullscale"]["ranks"]["kxx_s"]) == world
+        # the stencil and configs[2] come before the full-scale legs (a cut tail keeps them)
+        keys = list(line)
+        assert keys.index("conv_stencil_roofline") < keys.index("fullscale")
+        assert keys.index("mnist_as_tf") < keys.index("fullscale")
+
+
+def test_line_keeps_leg_errors_short():
+    import json
+    b = _bench()
+    full = _recorded_full(8)
+    full["fullscale"] = {"error": {str(r): "RuntimeError: " + "x" * 900 for r in range(8)}}
+    full["cifar10"] = {"error": "skipped: budget (430 s used, ~40 s needed, 420 s allowed)"}
+    line = b.compact_line(full)
+    assert "skipped: budget" in line["cifar10"]["error"]
+    assert len(json.dumps(line)) < b.LINE_MAX_CHARS
+
+
+def test_budget_skips_legs_that_would_start_late():
+    b = _bench()
+    d = b.Deadline(budget_s=10.0, hard_s=20.0)
+    legs = b.Legs(deadline=d)
+    assert legs.run("short", lambda: 1, est_s=1) == 1
+    out = legs.run("long", lambda: 2, est_s=30)
+    assert "skipped: budget" in out["error"]
+    d.t0 -= 11                                     # 11 s into the run
+    assert "skipped: budget" in legs.run("any", lambda: 3)["error"]
+
+
+def _hang_worker(rank, world, port, q, hard_s):
+    """rank 1 blocks for good inside leg "b"; rank 0 waits for it in the leg's status
+    exchange until its watchdog prints the line at the hard limit"""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["CGP_BENCH_HANG_LEG"] = "b:1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = _bench()
+    t0 = time.monotonic()
+    d = b.Deadline(budget_s=hard_s / 2, hard_s=hard_s)
+    legs = b.Legs(world, rank, dist.new_group(backend="gloo"), d)
+    full = {"value": 1.0e8, "metric": "m"}
+    if rank == 0:
+        em = b.Emitter(write=lambda s: q.put(("line", s, time.monotonic() - t0)))
+        dog = b.Watchdog(d, em, lambda watchdog=False: b.compact_line(
+            dict(full, watchdog=f"leg {legs.current!r}" if watchdog else None)),
+            exit_fn=lambda: (q.close(), q.join_thread(), os._exit(3)))
+        dog.start()
+    full["a"] = legs.run("a", lambda: "a")
+    full["b"] = legs.run("b", lambda: "b")        # rank 1 never returns from this leg
+    q.put(("end", rank, time.monotonic() - t0))   # not reached by either rank
+
+
+def test_watchdog_prints_the_line_when_a_rank_hangs():
+    import json
+    world, hard_s = 2, 8.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hang_worker, args=(r, world, port, q, hard_s))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        kind, s, t = q.get(timeout=120)
+        assert kind == "line"
+        line = json.loads(s)
+        assert line["value"] == 100000000
+        assert "'b'" in line["watchdog"]
+        assert t < hard_s + 5, t                  # printed at the hard limit, not later
+        procs[0].join(timeout=30)
+        assert procs[0].exitcode == 3
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+            p.join(timeout=30)

@@ -47,6 +47,11 @@ def main(path):
                 print("    split", {x: v for x, v in f["solve_split"].items() if x != "note"})
             for rk in f.get("ranks") or []:
                 print("    rank", rk)
+    di = d.get("dropin")
+    if di:
+        print("  dropin", di)
+    if d.get("watchdog"):
+        print("  WATCHDOG", d["watchdog"])
     f32 = d.get("f32")
     if f32:
         print("  f32", {k: (v.get("value") if isinstance(v, dict) else None)
