@@ -48,8 +48,36 @@ class _ImageVariances:
         return len(self.images)
 
 
+# bumped by every change an NNGPKernel's structure key could see (attribute sets and
+# deletes, add_module / register_buffer, .to() / .double() / .cuda() through _apply):
+# _structure_key reuses its last walk while the generation is unchanged
+_GENERATION = [0]
+
+
 class NNGPKernel(nn.Module):
     """Base class; ``forward`` mirrors kernels.py:18-57."""
+
+    def __setattr__(self, name, value):
+        _GENERATION[0] += 1
+        super().__setattr__(name, value)
+
+    def __delattr__(self, name):
+        _GENERATION[0] += 1
+        super().__delattr__(name)
+
+    def add_module(self, name, module):
+        _GENERATION[0] += 1
+        super().add_module(name, module)
+
+    def register_buffer(self, name, tensor, persistent=True):
+        _GENERATION[0] += 1
+        super().register_buffer(name, tensor, persistent)
+
+    def _apply(self, fn, *args, **kwargs):
+        _GENERATION[0] += 1
+        out = super()._apply(fn, *args, **kwargs)
+        _GENERATION[0] += 1
+        return out
 
     def _plan(self, h: int, w: int) -> Plan:
         cache = self.__dict__.setdefault("_cgp_plans", {})
@@ -63,18 +91,38 @@ class NNGPKernel(nn.Module):
         return plan
 
     def _structure_key(self):
-        """Changes whenever a hyper-parameter the program depends on changes."""
+        """Changes whenever a hyper-parameter the program depends on changes.  Asked on
+        every forward (the plan cache's key): ``modules()`` over the 114-module ResNets
+        cost a quarter of a millisecond per call, as long as a B = 200 tile's kernels
+        (bench.py ``dropin``).  So the last key is reused while no NNGPKernel has changed
+        since (_GENERATION; a tree with a Mixture is walked every time, its logits can
+        change in place), and the walk itself goes by hand (pre-order, attributes read
+        from the instance dicts)."""
+        memo = self.__dict__.get("_cgp_skey")
+        if memo is not None and memo[0] == _GENERATION[0]:
+            return memo[1]
+        gen = _GENERATION[0]
+        mixture = False
         key = []
-        for m in self.modules():
+        stack = [self]
+        while stack:
+            m = stack.pop()
+            d = m.__dict__
             if isinstance(m, Conv2d):
                 # host-side attributes only: reading the (device) buffer would sync
-                key.append(("c", m.kernel_size, m.stride, m.padding, m.dilation,
-                            float(m.var_weight), float(m.var_bias), m.kernel.dtype))
+                key.append(("c", d["kernel_size"], d["stride"], d["padding"], d["dilation"],
+                            float(d["var_weight"]), float(d["var_bias"]),
+                            d["_buffers"]["kernel"].dtype))
             elif isinstance(m, Mixture):
+                mixture = True
                 key.append(("m", tuple(m.proportions())))
             else:
-                key.append((type(m).__name__, len(getattr(m, "mods", ()))))
-        return tuple(key)
+                key.append((type(m).__name__, len(d.get("mods", ()))))
+            stack.extend(reversed(d["_modules"].values()))
+        key = tuple(key)
+        if not mixture:
+            self.__dict__["_cgp_skey"] = (gen, key)     # not through __setattr__
+        return key
 
     def set_fusion(self, enabled: bool):
         """Enable/disable op fusion in the pair pipeline (for A/B tests; default on)."""
@@ -154,7 +202,8 @@ class NNGPKernel(nn.Module):
             # every variance map in one launch (cgp_var_chain_*), quartered x-side copies
             # included (kernels.py:44-49 moments, then the program on each image)
             fused = plan.run_variances_fused(x, y, n1, n2, same, stream, net.need_var,
-                                             net.quarter_vars(x.dtype, plan.flags))
+                                             net.quarter_vars(x.dtype, plan.flags),
+                                             views=False)
             if fused is not None:
                 var, qvar = fused
                 return net.run(x, y, var, n1, n2, same, stream, plan.flags, qvar=qvar)

@@ -601,7 +601,49 @@ class NetPlan:
     def lds_bytes(self, itemsize: int) -> int:
         return self.lds_elems * itemsize
 
+    def _ops_template(self, sidx, stage, flags, itemsize):
+        """Stage ``sidx``'s op records with every field but the variance / state pointers
+        filled, built once per (stage, flags, itemsize): the bytes (numpy uint8), the
+        uint64 slots of the pointer fields with what each holds — (value, side) of the
+        variance maps, or "in" / "out" for the state buffers — and the compiled program
+        id (cgp_net_program compares only the non-pointer fields).  A forward per tile then
+        copies the bytes and writes the pointers: building the records field by field cost
+        ~0.15 ms per mnist_as_tf tile (tools/dropin_probe.py), a quarter of a B = 200
+        tile's kernel time."""
+        import numpy as np
+        key = (sidx, flags, itemsize)
+        cache = self.__dict__.setdefault("_templates", {})
+        t = cache.get(key)
+        if t is not None:
+            return t
+        arr = self._ops_array(stage, None)
+        size = ctypes.sizeof(N.NetOp)
+        slots, what = [], []
+        for k, (f, v) in enumerate(stage.records):
+            fields = {}                    # _ops_array's order: a state pointer wins
+            if v is not None:
+                fields.update(var_x=(v, 0), var_y=(v, 1))
+            if "var2" in f:
+                fields.update(var2_x=(f["var2"], 0), var2_y=(f["var2"], 1))
+            if f.get("state") in ("in", "out"):
+                fields["var_x"] = f["state"]
+            for name, src in fields.items():
+                off = k * size + getattr(N.NetOp, name).offset
+                assert off % 8 == 0
+                slots.append(off // 8)
+                what.append(src)
+        lib = N.load()
+        fl = flags | (N.CGP_FLAG_NET_DUAL if stage.dual else 0)
+        program = lib.cgp_net_program(ctypes.byref(arr), stage.n_ops, stage.pairs, fl,
+                                      stage.lds_elems, itemsize) if USE_PROGRAMS else 0
+        t = (np.frombuffer(bytes(arr), dtype=np.uint8).copy(), np.asarray(slots, np.int64),
+             what, program)
+        cache[key] = t
+        return t
+
     def _ops_array(self, stage, var, state_in=None, state_out=None):
+        """the stage's op records as a ctypes array; ``var`` None leaves the variance /
+        state pointers null (the template of _ops_template)"""
         arr = (N.NetOp * stage.n_ops)()
         for k, (f, v) in enumerate(stage.records):
             o = arr[k]
@@ -615,6 +657,8 @@ class NetPlan:
             o.weight, o.bias = f.get("weight", 0.0), f.get("bias", 0.0)
             o.dst2 = f.get("dst2", -1)
             o.zero_halo = _zero_code(f.get("zero")) | (_zero_code(f.get("zero2")) << 16)
+            if var is None:
+                continue
             if v is not None:
                 vx, vy = var[v]
                 o.var_x, o.var_y = vx.data_ptr(), vy.data_ptr()
@@ -689,12 +733,18 @@ class NetPlan:
                 keep.append(q)
                 var[v] = (q, vy)
         for sidx, st in enumerate(self.stages):
-            arr = self._ops_array(st, var, states[sidx], states[sidx + 1])
+            tmpl, slots, what, program = self._ops_template(sidx, st, flags, x.element_size())
+            ptrs = [var[w[0]][w[1]].data_ptr() if isinstance(w, tuple) else
+                    (states[sidx] if w == "in" else states[sidx + 1]).data_ptr()
+                    for w in what]
             # pinned + non_blocking: a pageable H2D copy would block the host until the
             # previous tile's kernels drained, leaving the GPU idle while this tile's small
             # launches are issued; the caching host allocator keeps the pinned block until
             # the copy has run
-            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).pin_memory()
+            host = torch.empty((len(tmpl),), dtype=torch.uint8, pin_memory=True)
+            hb = host.numpy()
+            hb[:] = tmpl
+            hb.view("<u8")[slots] = ptrs
             ops_dev = host.to(x.device, non_blocking=True)   # stream-ordered, freed stream-ordered
             keep.append(ops_dev)
             a = N.NetArgs()
@@ -709,9 +759,7 @@ class NetPlan:
             a.flags = flags | (N.CGP_FLAG_NET_DUAL if st.dual else 0)
             a.pairs = st.pairs
             a.final_stage = int(st.final)
-            a.program = lib.cgp_net_program(ctypes.byref(arr), st.n_ops, st.pairs, a.flags,
-                                            st.lds_elems, x.element_size()) \
-                if USE_PROGRAMS else 0
+            a.program = program
             launches.append(a)
 
         pairs = n1 * (n1 - 1) // 2 if same else n1 * n2

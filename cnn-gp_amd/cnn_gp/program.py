@@ -270,6 +270,18 @@ def _adjacent(x, y) -> bool:
             and y.data_ptr() == x.data_ptr() + x.numel() * x.element_size())
 
 
+
+class DevPtr:
+    """A device address inside ``base`` (kept alive by the handle, like a view would be):
+    what the launch records need of a variance map, without building a tensor view."""
+    __slots__ = ("base", "off")
+
+    def __init__(self, base: torch.Tensor, off: int):
+        self.base, self.off = base, off
+
+    def data_ptr(self) -> int:
+        return self.base.data_ptr() + self.off
+
 class Plan:
     """A compiled model at one input geometry: the variance program and the fused pair
     program.  Cached per (H, W, fuse) on the model."""
@@ -465,10 +477,12 @@ class Plan:
         cache[key] = chain
         return chain
 
-    def run_variances_fused(self, x, y, n1, n2, same, stream, need, quarter=()):
+    def run_variances_fused(self, x, y, n1, n2, same, stream, need, quarter=(), views=True):
         """run_variances in one launch.  Returns (var, qvar): var[v] = (xx [n1,..],
         yy [n2,..]) for v in need (yy is xx when same), qvar[v] = xx / 4 for v in quarter;
-        None when the chain kernel cannot run this program."""
+        None when the chain kernel cannot run this program.  ``views=False`` gives
+        DevPtr handles (data_ptr() only) instead of tensor views: a forward only needs the
+        maps' addresses, and ~90 views cost ~0.1 ms of host time per ResNet tile."""
         need = set(need)
         quarter = set(quarter) & need
         chain = self._var_chain(need, quarter, x.device)
@@ -490,6 +504,15 @@ class Plan:
                 "cgp_var_chain")
         shapes = self.prog.shapes
         var, qvar = {}, {}
+        if not views:
+            item = out.element_size()
+            for v, off in chain["store"].items():
+                ho, wo = shapes[v]
+                px = DevPtr(out, n * off * item)
+                var[v] = (px, px if same else DevPtr(out, (n * off + n1 * ho * wo) * item))
+            for v, off in chain["qstore"].items():
+                qvar[v] = DevPtr(out, (n * chain["total"] + n1 * off) * item)
+            return var, qvar
         for v, off in chain["store"].items():
             ho, wo = shapes[v]
             blk = out[n * off:n * (off + ho * wo)].view(n, ho, wo)

@@ -911,3 +911,31 @@ def test_bound_build_exact_relu_and_checks():
         m.tile_from_variances(vx, 0, 10, vx, 5, 5, False)
     # maps larger than the caller's budget: no bound build (the builders go per tile)
     assert m.image_variances(X, max_bytes=1024) is None
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_var_chain_pointer_handles_match_views(same):
+    """forward() hands the launch records DevPtr handles instead of tensor views
+    (program.Plan.run_variances_fused(views=False)): every handle is the address of the
+    view the tensor form builds, on the same chain output layout"""
+    m = configs_util.model("mnist_as_tf").to(DEV, torch.float64)
+    plan = m._plan(28, 28)
+    net = m._net_plan(plan, 8)
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand((5, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    y = x if same else torch.rand((3, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    q = net.quarter_vars(torch.float64, plan.flags)
+    torch.manual_seed(0)
+    v1, q1 = plan.run_variances_fused(x, y, len(x), len(y), same, s, net.need_var, q)
+    v2, q2 = plan.run_variances_fused(x, y, len(x), len(y), same, s, net.need_var, q,
+                                      views=False)
+    assert v1.keys() == v2.keys() and q1.keys() == q2.keys()
+    base1 = next(iter(v1.values()))[0].untyped_storage().data_ptr()
+    base2 = next(iter(v2.values()))[0].base.data_ptr()
+    for v in v1:
+        for a, b in zip(v1[v], v2[v]):
+            assert a.data_ptr() - base1 == b.data_ptr() - base2
+    for v in q1:
+        assert q1[v].data_ptr() - base1 == q2[v].data_ptr() - base2
+    torch.cuda.synchronize()

@@ -421,3 +421,62 @@ def test_program_match_ignores_weights_but_not_structure():
                                st.lds_elems, 8) == 0
     assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops, np_, 0, st.lds_elems + 2, 8) == 0
     assert lib.cgp_net_program(ctypes.byref(arr), st.n_ops - 1, np_, 0, st.lds_elems, 8) == 0
+
+
+def test_tensor_rows_equals_dataloader_collation():
+    """ProductIterator's sliced batches (data.tensor_rows) are exactly what the
+    reference's DataLoader collation of the same Subset yields (data.py:36-96), for the
+    dataset shapes DatasetFromConfig builds (Subset of a ConcatDataset, across the
+    train/test boundary) and for index lists; other datasets fall back to the DataLoader."""
+    from torch.utils.data import ConcatDataset, DataLoader, Subset, TensorDataset
+    from cnn_gp.data import ProductIterator, tensor_rows
+    g = torch.Generator().manual_seed(0)
+    a = TensorDataset(torch.rand((50, 1, 4, 4), generator=g), torch.arange(50))
+    b = TensorDataset(torch.rand((30, 1, 4, 4), generator=g), torch.arange(100, 130))
+    cat = ConcatDataset([a, b])
+
+    def ref(ds, lo, hi):
+        return next(iter(DataLoader(Subset(ds, range(lo, hi)), batch_size=hi - lo)))
+    cases = [(a, 0, 50), (a, 7, 19), (cat, 40, 60), (cat, 50, 80), (cat, 0, 80),
+             (Subset(cat, range(45, 75)), 3, 17), (Subset(a, [3, 1, 4, 1, 5]), 1, 4)]
+    for ds, lo, hi in cases:
+        got, want = tensor_rows(ds, lo, hi), ref(ds, lo, hi)
+        assert len(got) == len(want) == 2
+        for x, y in zip(got, want):
+            assert x.dtype == y.dtype and torch.equal(x, y)
+
+    class Plain(torch.utils.data.Dataset):
+        def __len__(self):
+            return 5
+
+        def __getitem__(self, k):
+            return torch.full((1, 2, 2), float(k)), k
+    assert tensor_rows(Plain(), 0, 5) is None
+    for ds in (cat, Plain()):
+        for same, (i, x), (j, x2) in ProductIterator(16, ds, None):
+            want = ref(ds, i, min(i + 16, len(ds)))[0]
+            assert torch.equal(x[0], want)
+
+
+@pytest.mark.parametrize("name", ["mnist_paper_convnet_gp", "mnist_as_tf", "cifar10"])
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_op_record_template_equals_records_built_per_call(name, dt):
+    """NetPlan.prepare writes each forward's op records from a cached template plus the
+    variance / state pointers (_ops_template): byte-identical to building every record
+    field by field (_ops_array), and the same compiled program id"""
+    ids, net = _stage_program_ids(name, dt)
+    itemsize = torch.tensor([], dtype=dt).element_size()
+    # distinct fake maps per value and side, distinct state buffers
+    var = {v: (torch.empty(4 + 2 * k), torch.empty(5 + 2 * k))
+           for k, v in enumerate(sorted(net.need_var))}
+    states = [torch.empty(7 + k) for k in range(len(net.stages) + 1)]
+    for sidx, st in enumerate(net.stages):
+        flags = 0
+        tmpl, slots, what, program = net._ops_template(sidx, st, flags, itemsize)
+        ptrs = [var[w[0]][w[1]].data_ptr() if isinstance(w, tuple) else
+                (states[sidx] if w == "in" else states[sidx + 1]).data_ptr() for w in what]
+        buf = tmpl.copy()
+        buf.view("<u8")[slots] = ptrs
+        ref = net._ops_array(st, var, states[sidx], states[sidx + 1])
+        assert bytes(buf) == bytes(ref)
+        assert program == ids[sidx]
