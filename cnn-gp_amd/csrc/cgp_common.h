@@ -188,9 +188,11 @@ static __constant__ PolyCoef kReluPolyTabD = poly_coef(false);
 static __constant__ PolyCoef kReluPolyTabDq = poly_coef(true);
 
 // Range-adaptive ReLU: lower-degree fits of P on x in [0, kReluAdaptX0/1/2] = [0, 1/8],
-// [0, 1/4], [0, 3/8] (degrees 7, 9, 11) at the error bound of the full degree-13 fit
-// (5.8e-15 / 8.2e-15 / 8.6e-15 vs 1.6e-14; tools/fit_relu_poly.py ADAPT), quartered like
-// kReluPolyTabDq.  relu_q_n takes the shortest one whose interval holds every pixel of its
+// [0, 1/4], [0, 3/8], quartered like kReluPolyTabDq.  Default (CGP_RELU_TOL=1, round 5):
+// degrees 6, 8, 9 and 11 on [0, 1/2], every fit within 1e-12 of the exact map (2.2e-13 /
+// 1.3e-13 / 9.2e-13 / 7.6e-13; ConvNet +2%, mnist_as_tf +1-2.5%, cifar10 +2%,
+// profiles/r5/ab_r5d_relu_tol.log); CGP_RELU_TOL=0: degrees 7, 9, 11, 13 at 1.6e-14
+// (tools/fit_relu_poly.py ADAPT / ADAPT_TOL).  relu_q_n takes the shortest one whose interval holds every pixel of its
 // vote group (a uniform branch).  Deep layers have |rho| near 1 (x small): on MNIST-like
 // pairs the ConvNet's ReLUs 2-7 have x <= 0.24 and its last four x <= 0.125.
 // Measured and not kept: every degree 6-13 by a binary search of votes, one

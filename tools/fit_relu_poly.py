@@ -118,6 +118,11 @@ def check(monox, dt, npts=20001, xmax=0.5):
 # range-adaptive ReLU (CGP_RELU_ADAPT): lower degrees on sub-intervals [0, xmax] with the
 # same 1.6e-14 bound, taken by a wave whose every pixel has x <= xmax (relu_q_n)
 ADAPT = ((0.125, 7), (0.25, 9), (0.375, 11))
+# CGP_RELU_TOL=1: the same intervals at a 1e-12 bound (6 / 8 / 9, and 11 on [0, 1/2]:
+# 2.2e-13 / 1.3e-13 / 9.2e-13 / 7.6e-13), 3-5 decades inside the end-to-end parity bounds
+#  and 4 inside the reference's own acos noise near |rho| = 1
+ADAPT_TOL = ((0.125, 6), (0.25, 8), (0.375, 9))
+DEG_TOL = 11
 # ... and for the float polynomial (its bound: the degree-6 fit's 7.9e-8)
 ADAPT_F = ((0.125, 3), (0.375, 5))
 # every degree 6-12 on [0, xmax] at or below the degree-13 fit's bound, the degree-13
@@ -138,6 +143,8 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
         dbl[d] = check(to_x(fit(d)), np.float64, npts=4001)
     sub = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
            for xm, d in ADAPT]
+    sub_tol = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
+               for xm, d in ADAPT_TOL]
     sub_f = [(xm, d, check(to_x(fit(d, xm), xm), np.float32, npts=4001, xmax=xm))
              for xm, d in ADAPT_F]
     chain = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
@@ -146,12 +153,23 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
         "// relu_poly.h - generated by tools/fit_relu_poly.py --write (do not edit by hand).",
         "// P(x), x = (1 - |rho|)/2 in [0, 1/2], monomials in x; the fast ReLU covariance map is",
         "//   out = max(c, 0)/2 + sqrt(t) * x * sqrt(x) * P(x)",
-        f"// double: degree {deg_d} (CGP_RELU_DEG_D selects "
+        f"// double, on [0, 1/2] (CGP_RELU_DEG_D selects "
         + ", ".join(f"{d}: {dbl[d][0]:.2e}" for d in sorted(dbl)) + " max rel err);",
         f"// float: degree {deg_f}, max rel err {ef:.2e}",
         "#pragma once",
+        "// CGP_RELU_TOL=1 (default): the 1e-12 tables (degree " + str(DEG_TOL)
+        + " on [0, 1/2], adaptive " + " / ".join(str(d) for _, d in ADAPT_TOL)
+        + "); CGP_RELU_TOL=0: the 1.6e-14 tables (degree " + str(deg_d) + ", adaptive "
+        + " / ".join(str(d) for _, d in ADAPT) + ")",
+        "#ifndef CGP_RELU_TOL",
+        "#define CGP_RELU_TOL 1",
+        "#endif",
         "#ifndef CGP_RELU_DEG_D",
+        "#if CGP_RELU_TOL",
+        f"#define CGP_RELU_DEG_D {DEG_TOL}",
+        "#else",
         f"#define CGP_RELU_DEG_D {deg_d}",
+        "#endif",
         "#endif",
     ]
     for k, d in enumerate(sorted(dbl)):
@@ -161,13 +179,16 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
         lines += [f"    {float(c)!r}," for c in dbl[d][1]]
         lines += ["};"]
     lines += ["#else", "#error \"CGP_RELU_DEG_D: no table for this degree\"", "#endif"]
-    for k, (xm, d, (err, cfs)) in enumerate(sub):
-        lines += [f"// x in [0, {xm}]: degree {d}, max rel err {err:.2e}",
-                  f"constexpr double kReluAdaptX{k} = {xm!r};",
-                  f"constexpr int kReluAdaptDeg{k} = {d};",
-                  f"constexpr double kReluAdaptP{k}[{d + 1}] = {{"]
-        lines += [f"    {float(c)!r}," for c in cfs]
-        lines += ["};"]
+    for tag, rows in (("#if CGP_RELU_TOL", sub_tol), ("#else", sub)):
+        lines += [tag]
+        for k, (xm, d, (err, cfs)) in enumerate(rows):
+            lines += [f"// x in [0, {xm}]: degree {d}, max rel err {err:.2e}",
+                      f"constexpr double kReluAdaptX{k} = {xm!r};",
+                      f"constexpr int kReluAdaptDeg{k} = {d};",
+                      f"constexpr double kReluAdaptP{k}[{d + 1}] = {{"]
+            lines += [f"    {float(c)!r}," for c in cfs]
+            lines += ["};"]
+    lines += ["#endif"]
     for k, (xm, d, (err, cfs)) in enumerate(sub_f):
         lines += [f"// float, x in [0, {xm}]: degree {d}, max rel err {err:.2e}",
                   f"constexpr float kReluAdaptFX{k} = {xm!r}f;",
