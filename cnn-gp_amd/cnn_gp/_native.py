@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 9
+CGP_ABI_VERSION = 10
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -138,6 +138,8 @@ SIGNATURES = {
     "cgp_chol_solve_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,
                                   ctypes.POINTER(_i64), _vp]),
     "cgp_chol_last_phases": (_i32, [_vp, ctypes.POINTER(_f64)]),
+    "cgp_chol_solve_f64_timed": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,
+                                        ctypes.POINTER(_i64), ctypes.POINTER(_f64), _vp]),
     "cgp_gemm_f64": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_pred_var_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp]),
@@ -150,6 +152,8 @@ SIGNATURES = {
     "cgp_net_args_size": (ctypes.c_size_t, []),
     "cgp_net_occupancy": (_i32, [_i32, _i32, _i32, _i32]),
     "cgp_net_program": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32]),
+    "cgp_net_validate": (_i32, [_vp, _i32, _i32]),
+    "cgp_net_static_lds": (_i32, []),
     "cgp_net_f64": (_i32, [ctypes.POINTER(NetArgs), _vp]),
     "cgp_net_f32": (_i32, [ctypes.POINTER(NetArgs), _vp]),
     "cgp_var_op_size": (ctypes.c_size_t, []),

@@ -37,7 +37,8 @@ def _to_device(t: torch.Tensor, device) -> torch.Tensor:
 class _ImageVariances:
     """Variance maps of one image set for one Gram build (NNGPKernel.image_variances):
     var[v] = [N, h, w] maps of every value the whole-network kernel reads, qvar[v] their
-    quartered x-side copies (fp64 closed-form ReLU), key = (H, W, dtype, plan flags)."""
+    x-side copies scaled by cgp_net_xvar_scale() = 1/16 (fp64 closed-form ReLU), key =
+    (H, W, dtype, plan flags)."""
 
     __slots__ = ("images", "var", "qvar", "key")
 
@@ -199,7 +200,7 @@ class NNGPKernel(nn.Module):
         lib = N.load()
         net = None if diag else self._net_plan(plan, x.element_size())
         if net is not None and VAR_CHAIN:
-            # every variance map in one launch (cgp_var_chain_*), quartered x-side copies
+            # every variance map in one launch (cgp_var_chain_*), scaled (1/16) x-side copies
             # included (kernels.py:44-49 moments, then the program on each image)
             fused = plan.run_variances_fused(x, y, n1, n2, same, stream, net.need_var,
                                              net.quarter_vars(x.dtype, plan.flags),

@@ -50,7 +50,8 @@ USE_PROGRAMS = os.environ.get("CGP_NET_PROGRAMS", "1") != "0"
 # CGP_NET_CODE_FROM_SUM; one pair per workgroup or half): no map store, no map re-read,
 # one barrier less per pair.  CGP_NET_FUSE_REDUCE=0 keeps the two ops apart.
 FUSE_REDUCE = os.environ.get("CGP_NET_FUSE_REDUCE", "1") != "0"
-# quartered x-side variance maps for the fp64 closed-form ReLU (relu_q_n); 0 only to time
+# scaled (cgp_net_xvar_scale() = 1/16) x-side variance maps for the fp64 closed-form ReLU
+# (relu_q_n; "quarter" names the round-2 1/4 scale); 0 only to time
 # library builds that predate it (tools/variants.sh)
 QUARTER_MAPS = os.environ.get("CGP_NET_QUARTER", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
@@ -206,7 +207,8 @@ class NetPlan:
                 if hi < len(lowered) else []
             st = self._lower(lowered, lo, hi, np_, ins, outs, last, dual, itemsize)
             # the two-pair workgroup holds cgp_net_units(2) one-pair arenas
-            if np_ == 2 and st.lds_elems * itemsize * lib.cgp_net_units(2) > MAX_LDS_BYTES:
+            if np_ == 2 and st.lds_elems * itemsize * lib.cgp_net_units(2) > \
+                    MAX_LDS_BYTES - lib.cgp_net_static_lds():
                 st = self._lower(lowered, lo, hi, 1, ins, outs, last, dual, itemsize)
             self.stages.append(st)
         self.need_var = {vf}
@@ -508,7 +510,8 @@ class NetPlan:
                 f["code"] = lib.cgp_net_resolution(f["h"], f["w"])
             elif f["kind"] in (N.CGP_NET_MOMENTS, N.CGP_NET_LINEAR):
                 f["code"] = -1
-        if top * itemsize * lib.cgp_net_units(pairs) > MAX_LDS_BYTES:
+        # the kernel's static LDS (cgp_net_static_lds) sits beside the arenas
+        if top * itemsize * lib.cgp_net_units(pairs) > MAX_LDS_BYTES - lib.cgp_net_static_lds():
             if pairs == 1:
                 raise Unsupported(f"LDS footprint {top * itemsize} B")
         return Stage(records=recs, lds_elems=top, final_slot=final_origin, pairs=pairs,
@@ -617,6 +620,10 @@ class NetPlan:
         if t is not None:
             return t
         arr = self._ops_array(stage, None)
+        lib = N.load()
+        # the SUM / FROM_SUM contract (cnngp.h), checked on the host copy once per stage
+        N.check(lib.cgp_net_validate(ctypes.byref(arr), stage.n_ops, stage.pairs),
+                "cgp_net_validate")
         size = ctypes.sizeof(N.NetOp)
         slots, what = [], []
         for k, (f, v) in enumerate(stage.records):
@@ -632,7 +639,6 @@ class NetPlan:
                 assert off % 8 == 0
                 slots.append(off // 8)
                 what.append(src)
-        lib = N.load()
         fl = flags | (N.CGP_FLAG_NET_DUAL if stage.dual else 0)
         program = lib.cgp_net_program(ctypes.byref(arr), stage.n_ops, stage.pairs, fl,
                                       stage.lds_elems, itemsize) if USE_PROGRAMS else 0
@@ -694,7 +700,7 @@ class NetPlan:
     def prepare(self, x, y, var, n1: int, n2: int, same: bool, flags: int = 0,
                 out: Optional[torch.Tensor] = None, qvar: Optional[dict] = None):
         """Upload the op lists for these variance maps; return (launch(stream), out).
-        ``qvar``: the quartered x-side maps (program.Plan.run_variances_fused), else they
+        ``qvar``: the scaled (1/16) x-side maps (program.Plan.run_variances_fused), else they
         are filled here with cgp_scale_batch_f64.
         ``out`` may be a row-strided view (e.g. a tile of a larger K): the kernel writes
         K[i, j] at out[i * out.stride(0) + j]."""
@@ -717,8 +723,8 @@ class NetPlan:
         launches = []
         keep = []
         # the fp64 closed-form ReLU (csrc/cgp_common.h relu_q_n) reads the x-side variance
-        # maps quartered (an exact scaling that folds its Newton steps' halvings); the
-        # copies are filled on the launch stream before the kernels
+        # maps scaled by cgp_net_xvar_scale() = 1/16 (an exact scaling that folds its Newton
+        # steps' halvings); the copies are filled on the launch stream before the kernels
         quarters = []
         used = self.quarter_vars(x.dtype, flags)
         if used:

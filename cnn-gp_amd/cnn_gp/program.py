@@ -479,7 +479,8 @@ class Plan:
 
     def run_variances_fused(self, x, y, n1, n2, same, stream, need, quarter=(), views=True):
         """run_variances in one launch.  Returns (var, qvar): var[v] = (xx [n1,..],
-        yy [n2,..]) for v in need (yy is xx when same), qvar[v] = xx / 4 for v in quarter;
+        yy [n2,..]) for v in need (yy is xx when same), qvar[v] = xx scaled by
+        cgp_net_xvar_scale() (1/16 from ABI 9; "quarter" is the round-2 name) for v in quarter;
         None when the chain kernel cannot run this program.  ``views=False`` gives
         DevPtr handles (data_ptr() only) instead of tensor views: a forward only needs the
         maps' addresses, and ~90 views cost ~0.1 ms of host time per ResNet tile."""

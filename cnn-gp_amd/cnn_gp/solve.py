@@ -8,6 +8,7 @@ triangle the reference's HDF5 files fill — then dpotrs_64.  All through libcnn
 from __future__ import annotations
 
 import ctypes
+from typing import Optional
 
 import numpy as np
 import torch
@@ -63,8 +64,12 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
         s = _stream(dev)
         N.call("cgp_transpose_f64", N.ptr(yd), n, nrhs, N.ptr(bt), s)
         info = N._i64(0)
-        N.check(N.load().cgp_chol_solve_f64(N.ptr(K), n, n, N.ptr(bt), nrhs, n, float(jitter),
-                                            ctypes.byref(info), s), "cgp_chol_solve_f64")
+        ms = (N._f64 * 3)(-1.0, -1.0, -1.0)
+        _PHASES.pop(_dev_key(dev), None)        # a failing solve leaves no phases behind
+        N.check(N.load().cgp_chol_solve_f64_timed(N.ptr(K), n, n, N.ptr(bt), nrhs, n,
+                                                  float(jitter), ctypes.byref(info), ms, s),
+                "cgp_chol_solve_f64")
+        _PHASES[_dev_key(dev)] = tuple(ms)
         if info.value > 0:
             raise np.linalg.LinAlgError(
                 f"Kxx is not positive definite (leading minor of order {info.value})")
@@ -74,13 +79,25 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
     return sol.to(Y.device)
 
 
-def solve_phases(device=None) -> dict:
+# the phases of the last solve_system per device, as that call's own timed solve returned
+# them (cgp_chol_solve_f64_timed: taken under the solver's device lock, so a solve on
+# another thread cannot swap them); dropped at the start of every solve_system
+_PHASES = {}
+
+
+def _dev_key(dev) -> int:
+    dev = torch.device(dev)
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def solve_phases(device=None) -> Optional[dict]:
     """Seconds spent in the phases of the last solve_system on ``device`` (HIP events on
-    its stream, cgp_chol_last_phases): jitter (diag_add), factor (the Cholesky), potrs."""
+    its stream): jitter (diag_add), factor (the Cholesky), potrs — or None when the last
+    solve_system there raised before its solve was timed (or none ran)."""
     dev = torch.device(device) if device is not None else _device()
-    ms = (N._f64 * 3)()
-    with torch.cuda.device(dev):
-        N.check(N.load().cgp_chol_last_phases(_stream(dev), ms), "cgp_chol_last_phases")
+    ms = _PHASES.get(_dev_key(dev))
+    if ms is None or min(ms) < 0:
+        return None
     return {"jitter_s": ms[0] * 1e-3, "factor_s": ms[1] * 1e-3, "potrs_s": ms[2] * 1e-3}
 
 

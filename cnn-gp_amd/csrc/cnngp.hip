@@ -1528,6 +1528,14 @@ int cgp_transpose_f64(const double* src, int64_t rows, int64_t cols, double* dst
 
 int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
                        int64_t ldb, double jitter, int64_t* info, void* stream) {
+    return cgp_chol_solve_f64_timed(k, n, ldk, bt, nrhs, ldb, jitter, info, nullptr, stream);
+}
+
+int cgp_chol_solve_f64_timed(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
+                             int64_t ldb, double jitter, int64_t* info, double* phase_ms,
+                             void* stream) {
+    if (phase_ms)
+        for (int q = 0; q < 3; ++q) phase_ms[q] = -1.0;   // no phases unless the solve ran
     if (!k || !bt || !info) return fail(CGP_EINVAL, "chol_solve: NULL argument");
     if (n <= 0 || ldk < n || nrhs <= 0 || ldb < n)
         return fail(CGP_EINVAL, "chol_solve: bad sizes n=%lld ldk=%lld nrhs=%lld ldb=%lld",
@@ -1579,6 +1587,7 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
         float ms = 0.f;
         CGP_HIP(hipEventElapsedTime(&ms, b->ev[q], b->ev[q + 1]));
         b->phase_ms[q] = ms;
+        if (phase_ms) phase_ms[q] = ms;    // this call's own phases, under the device lock
     }
     b->timed = true;
     return CGP_OK;

@@ -260,6 +260,10 @@ struct NetP {
 // The pairs an op works on.  NP == 1: (i, j), uniform.  NP > 1: pair q of the group is
 // (tab[q], tab[kMaxNP + q]) from the workgroup's pair table in LDS, unit u0 + q.
 constexpr int kMaxNP = 16;
+// LDS the kernel declares statically (pair table, SUM partials, program records, the
+// work-counter slots) on top of the dynamic arenas: every LDS check (net_impl, net_wpe,
+// cgp_net_static_lds for the host's planner) counts this reserve
+constexpr long long kStaticLds = 1536;
 struct Pairs {
     unsigned i, j;
     const unsigned* tab;
@@ -286,9 +290,10 @@ __device__ __forceinline__ T relu_of(T c, T v1, T v2, const PolyTab& tab) {
     else
         return relu_fast(c, v1, v2, tab);
 }
-// The fp64 closed form reads quartered x-side variance maps (relu_q_n; the host passes
-// v/4 maps for f64 launches without CGP_FLAG_EXACT_RELU) and, when the producing conv
-// scaled its weight and bias by 1/4 (QIN), a quartered input.
+// The fp64 closed form reads scaled x-side variance maps (relu_q_n: the host passes
+// v × cgp_net_xvar_scale() = v/16 from ABI 9, v/4 before, for f64 launches without
+// CGP_FLAG_EXACT_RELU) and, when the producing conv scaled its weight and bias by 1/4
+// (QIN), a quartered input.
 template <typename T, bool EX>
 constexpr bool kQuarter = !EX && sizeof(T) == 8;
 
@@ -1193,7 +1198,14 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     const int tid = threadIdx.x;
     constexpr int UN = kUnitsOf<NP>;
     for (int e = tid; e < UN * p.lds_elems; e += kNTof<NP>) lds[e] = T(0);   // halos stay zero
+    // a FROM_SUM reduction reads these: zeroed, so an op list that breaks the SUM / FROM_SUM
+    // contract (cgp_net_validate) reads zeros, never another launch's LDS
+    if (tid < UN * (kNT / 64)) red_part[tid] = T(0);
     __shared__ ProgRec prog_recs[kRecsOf<PID>];
+    __shared__ long long next_u[2];
+    static_assert(sizeof(pair_tab) + sizeof(red_part) + sizeof(prog_recs) + sizeof(next_u) <=
+                      kStaticLds,
+                  "static LDS beyond the reserve the host checks count (kStaticLds)");
     if constexpr (PID >= 0) {
         for (int k = tid; k < kRecsOf<PID>; k += kNTof<NP>) {
             const cgp_net_op& r = p.ops[k];
@@ -1213,9 +1225,8 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     // flight on an XCD stay one contiguous window (a few supertiles) whose images and
     // variance maps its L2 holds; a static stride lets workgroups drift apart and the
     // window (and L2 misses) grow.  The next group's index is fetched one pair ahead.
-    // two slots used alternately: a slot is rewritten two advances later, after every
-    // thread has passed the barrier of the advance in between, so one barrier suffices
-    __shared__ long long next_u[2];
+    // two slots used alternately (next_u): a slot is rewritten two advances later, after
+    // every thread has passed the barrier of the advance in between, so one barrier suffices
     int adv = 0;
     unsigned long long* ctr = p.work + xcd;
     unsigned long long grab = 0;   // thread 0: the counter value fetched one pair ahead
@@ -1347,7 +1358,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
 // waves per SIMD the LDS footprint of a workgroup allows (`waves` waves per workgroup,
 // 4 SIMDs per CU), clamped to the instantiated register targets 3..5
 constexpr int net_wpe(long long lds_bytes, int cap = 5, int waves = kNT / 64) {
-    const long long wg = (160LL * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
+    const long long wg = (160LL * 1024) / (lds_bytes + kStaticLds);
     const long long w = wg * waves / 4;
     return w < 3 ? 3 : (w > cap ? cap : (int)w);
 }
@@ -1539,7 +1550,7 @@ int net_impl(const cgp_net_args* a, void* stream) {
     if (a->channels <= 0 || a->h <= 0 || a->w <= 0)
         return fail(CGP_EINVAL, "net: bad image shape");
     const long long lds_bytes = (long long)a->lds_elems * (long long)sizeof(T);
-    if (a->lds_elems <= 0 || lds_bytes > 160 * 1024)
+    if (a->lds_elems <= 0 || lds_bytes + kStaticLds > 160 * 1024)
         return fail(CGP_EINVAL, "net: LDS footprint %lld bytes out of range", lds_bytes);
     if (a->final_slot < 0 || a->final_slot >= a->lds_elems || a->hs < 0 ||
         a->hs >= a->lds_elems || a->part < 0 || a->part + 2 > a->lds_elems)
@@ -1571,8 +1582,9 @@ int net_impl(const cgp_net_args* a, void* stream) {
     const int np = a->pairs <= 0 ? 1 : a->pairs;
     if (np != 1 && np != 2 && np != 4 && np != kMaxNP)
         return fail(CGP_EINVAL, "net: %d pairs per workgroup (1, 2, 4 or 16)", np);
-    if (lds_bytes * net_units(np) > 160 * 1024)
-        return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS", np, lds_bytes * net_units(np));
+    if (lds_bytes * net_units(np) + kStaticLds > 160 * 1024)
+        return fail(CGP_EINVAL, "net: %d pairs need %lld B LDS (+ %lld B static)", np,
+                    lds_bytes * net_units(np), kStaticLds);
     // multi-pair stages address a pair's variance maps (<= 8 * threads / np pixels) with
     // 32-bit byte offsets (VarSrc)
     if (np > 1 && (a->n1 > a->n2 ? a->n1 : a->n2) * (8LL * net_threads(np) / np) *
@@ -1636,6 +1648,59 @@ int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pai
     if (lds_bytes <= 0 || (long long)lds_bytes * pairs > 160 * 1024) return 0;
     return f64 ? net_occupancy_for<double>(lds_bytes, flags, pairs)
                : net_occupancy_for<float>(lds_bytes, flags, pairs);
+}
+
+int cgp_net_static_lds(void) { return (int)kStaticLds; }
+
+int cgp_net_validate(const cgp_net_op* ops, int32_t nops, int32_t pairs) {
+    if (!ops || nops <= 0) return fail(CGP_EINVAL, "net_validate: NULL or empty op list");
+    const int np = pairs <= 0 ? 1 : pairs;
+    auto geo = [](const cgp_net_op& r) -> const GeoRow* {
+        const int g = r.code & CGP_NET_CODE_GEOMETRY;
+        return r.kind == CGP_NET_CONV && r.code >= 0 && g < kNumGeo ? &kGeoTable[g] : nullptr;
+    };
+    for (int k = 0; k < nops; ++k) {
+        const cgp_net_op& r = ops[k];
+        const bool sum = r.kind == CGP_NET_CONV && r.code >= 0 && (r.code & CGP_NET_CODE_SUM);
+        const bool from = r.kind == CGP_NET_CONV && r.code >= 0 && (r.code & CGP_NET_CODE_FROM_SUM);
+        if (sum) {
+            const GeoRow* g = geo(r);
+            const bool point = g && g->taps == 1 && g->off == 0;
+            const bool reduce = g && g->ho == 1 && g->wo == 1 && g->off == 0 &&
+                                g->taps == g->h && g->taps == g->w;
+            if (!g || g->taps <= 3 || point || reduce)
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_SUM needs a separable "
+                                        "conv (more than 3 taps, not pointwise, not a reduction)", k);
+            if (r.add >= 0 || r.dst2 >= 0)
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_SUM with an addend or "
+                                        "a second output", k);
+            if (np > 2)
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_SUM in a %d-pair stage "
+                                        "(one pair per workgroup or half only)", k, np);
+            if (k + 1 >= nops || !(ops[k + 1].kind == CGP_NET_CONV && ops[k + 1].code >= 0 &&
+                                   (ops[k + 1].code & CGP_NET_CODE_FROM_SUM)) ||
+                ops[k + 1].src != r.dst)
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_SUM not followed by the "
+                                        "CGP_NET_CODE_FROM_SUM reduction of its map", k);
+            for (int m = k + 2; m < nops; ++m)
+                if (ops[m].src == r.dst || ops[m].add == r.dst)
+                    return fail(CGP_EINVAL, "net_validate: op %d reads the map of SUM op %d, "
+                                            "which is never stored", m, k);
+        }
+        if (from) {
+            const GeoRow* g = geo(r);
+            const bool reduce = g && g->ho == 1 && g->wo == 1 && g->off == 0 &&
+                                g->taps == g->h && g->taps == g->w;
+            if (!reduce || np > 2)
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_FROM_SUM needs a "
+                                        "one-pair full-map reduction", k);
+            if (k == 0 || !(ops[k - 1].kind == CGP_NET_CONV && ops[k - 1].code >= 0 &&
+                            (ops[k - 1].code & CGP_NET_CODE_SUM)))
+                return fail(CGP_EINVAL, "net_validate: op %d: CGP_NET_CODE_FROM_SUM without a "
+                                        "CGP_NET_CODE_SUM conv before it", k);
+        }
+    }
+    return CGP_OK;
 }
 
 int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t flags,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 9
+#define CGP_ABI_VERSION 10
 
 /* error codes */
 #define CGP_OK 0
@@ -206,6 +206,15 @@ int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nr
  */
 int cgp_chol_last_phases(void* stream, double* ms);
 /*
+ * ABI 10: cgp_chol_solve_f64 that also returns ITS OWN phase times in phase_ms[3] (ms:
+ * jitter, factor, potrs; NULL: none), taken under the device's solver lock — another
+ * thread's solve on the same device cannot overwrite them between the call and a later
+ * cgp_chol_last_phases.  phase_ms is -1 in every slot when the call fails before timing.
+ */
+int cgp_chol_solve_f64_timed(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
+                             int64_t ldb, double jitter, int64_t* info, double* phase_ms,
+                             void* stream);
+/*
  * Row-major C[m][n] = A[m][kdim] @ B[kdim][n] (fp64, rocBLAS) — the Kxz @ α product of
  * print_accuracy, classify_gp.py:39-42.
  */
@@ -269,12 +278,21 @@ int cgp_argmax_rows_f64(const double* a, int64_t rows, int64_t cols, int64_t* ou
  * first cells: separable row passes write their input rows there and a one-pair
  * full-map reduction its two wave partial sums. */
 #define CGP_NET_CODE_HS_CLEAN 0x100
-/* CONV code flags of a map that only a full-map reduction reads (ABI 9; one pair per
- * workgroup or half; the host sets both or neither):
+/* CONV code flags of a map that only a full-map reduction reads (ABI 9; the host sets
+ * both or neither):
  *   CGP_NET_CODE_SUM       a separable conv does not store its output map: each wave adds
  *                          its outputs (after the ReLU) into the pair's two wave partial sums
  *   CGP_NET_CODE_FROM_SUM  the next op, a full-map reduction (1x1 output, window = map) of
- *                          that map, reads those partial sums instead of the map */
+ *                          that map, reads those partial sums instead of the map
+ * Preconditions (cgp_net_validate checks them on a host copy of the op list; the kernels
+ * do not, since the list they read is in device memory):
+ *   - SUM only on a separable conv: more than 3 taps, not pointwise, not a full-map
+ *     reduction (the direct, pointwise and reduction forms store their map regardless);
+ *   - SUM with add < 0 and dst2 < 0 (the summed outputs are the conv+ReLU values only);
+ *   - one pair per workgroup or half (pairs 1 or 2): multi-pair stages ignore both flags;
+ *   - the op right after a SUM conv is the FROM_SUM reduction of its dst map, and no later
+ *     op reads that map (it is never stored); FROM_SUM only right after a SUM conv.
+ * A list that breaks them reads zeroed partial sums (deterministic, wrong). */
 #define CGP_NET_CODE_SUM 0x200
 #define CGP_NET_CODE_FROM_SUM 0x400
 #define CGP_NET_CODE_GEOMETRY 0xff  /* the cgp_net_geometry() code in the low bits */
@@ -403,7 +421,7 @@ int cgp_net_resolution(int32_t h, int32_t w);
 int cgp_net_occupancy(int32_t lds_bytes, int32_t f64, int32_t flags, int32_t pairs);
 /* LDS arenas (one per pair unit) a workgroup of `pairs` pairs holds: `pairs`, except for
  * the two-pair head stage, whose workgroup holds two one-pair slices.  A stage needs
- * lds_bytes × cgp_net_units(pairs) <= 160 KB. */
+ * lds_bytes × cgp_net_units(pairs) + cgp_net_static_lds() <= 160 KB. */
 int cgp_net_units(int32_t pairs);
 /* The compiled program (k > 0) whose op list equals ops[0, nops) (HOST memory) in every
  * field but weight, bias and the variance / state pointers, for `pairs` pairs per
@@ -412,6 +430,14 @@ int cgp_net_units(int32_t pairs);
  * (net_programs.h); a program kernel runs them with every offset an immediate. */
 int cgp_net_program(const cgp_net_op* ops, int32_t nops, int32_t pairs, int32_t flags,
                     int32_t lds_elems, int32_t itemsize);
+/* ABI 10: CGP_OK, or CGP_EINVAL (message in cgp_last_error) when the op list (HOST memory)
+ * breaks the CGP_NET_CODE_SUM / CGP_NET_CODE_FROM_SUM preconditions for `pairs` pairs per
+ * workgroup.  cnn_gp.netplan calls it once per stage before the first launch. */
+int cgp_net_validate(const cgp_net_op* ops, int32_t nops, int32_t pairs);
+/* ABI 10: bytes of LDS the fused kernel declares statically per workgroup (pair table, SUM
+ * partial sums, program records, work-counter slots), on top of lds_bytes ×
+ * cgp_net_units(pairs): a stage fits when the sum is <= 160 KB. */
+int cgp_net_static_lds(void);
 /* ABI 6: cgp_net_f64's fast path reads var_x / var2_x quartered (see cgp_net_op). */
 int cgp_net_f64(const cgp_net_args* args, void* stream);
 int cgp_net_f32(const cgp_net_args* args, void* stream);

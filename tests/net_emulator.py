@@ -68,11 +68,46 @@ def _relu(c, v1, v2):
         return (sin + (math.pi - np.arccos(cos)) * c) / (2 * math.pi)
 
 
+def validate(stage):
+    """The CGP_NET_CODE_SUM / FROM_SUM preconditions of include/cnngp.h (the library's
+    cgp_net_validate): ValueError for an op list the kernel would run into zeroed partial
+    sums."""
+    recs = [f for f, _ in stage.records]
+    for k, f in enumerate(recs):
+        code = f.get("code", 0)
+        if f["kind"] != 0 or code < 0:       # the flags are conv codes (LOAD / STORE use
+            continue                         # their code field for the record size)
+        h, w, ho, wo, taps, s, off = f["geom"]
+        point = taps == 1 and off == 0
+        reduce = ho == wo == 1 and off == 0 and taps == h == w
+        if code & SUM:
+            if taps <= 3 or point or reduce:
+                raise ValueError(f"op {k}: SUM needs a separable conv")
+            if f["add"] >= 0 or f.get("dst2", -1) >= 0:
+                raise ValueError(f"op {k}: SUM with an addend or a second output")
+            if stage.pairs > 2:
+                raise ValueError(f"op {k}: SUM in a {stage.pairs}-pair stage")
+            nxt = recs[k + 1] if k + 1 < len(recs) else None
+            if nxt is None or nxt["kind"] != 0 or not nxt.get("code", 0) & FROM_SUM or \
+                    nxt["src"] != f["dst"]:
+                raise ValueError(f"op {k}: SUM not followed by the FROM_SUM reduction of its map")
+            if any(g["src"] == f["dst"] or g["add"] == f["dst"] for g in recs[k + 2:]):
+                raise ValueError(f"op {k}: a later op reads the never-stored SUM map")
+        if code & FROM_SUM:
+            if not reduce or stage.pairs > 2:
+                raise ValueError(f"op {k}: FROM_SUM needs a one-pair full-map reduction")
+            prev = recs[k - 1] if k else None
+            if prev is None or prev["kind"] != 0 or prev.get("code", 0) < 0 or \
+                    not prev["code"] & SUM:
+                raise ValueError(f"op {k}: FROM_SUM without a SUM conv before it")
+
+
 def run_stage(stage, x_i, y_j, var, i, j, lds, state):
     """One pair through one stage's op list.  ``lds`` (this pair's arena) persists
     across the pairs a workgroup walks (the kernel zeroes it once per workgroup), so
     stale values of earlier pairs stay in every cell an op does not write — as on the
     device.  ``state``: {"in": record, "out": record} of this pair's unit."""
+    validate(stage)
     hs0 = 0
     fused = None               # the map sum a CGP_NET_CODE_SUM conv hands the next reduction
 

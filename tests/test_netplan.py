@@ -100,3 +100,62 @@ def test_conv_fused_into_final_reduction(cfg, fused, monkeypatch):
         X = rng.random((3, C, side, side))
         np.testing.assert_allclose(E.kernel(net, X, X, True), E.kernel(apart, X, X, True),
                                    rtol=1e-14)
+
+
+def test_sum_contract_is_validated():
+    """CGP_NET_CODE_SUM / FROM_SUM preconditions (include/cnngp.h): the lowered reference
+    programs pass cgp_net_validate and the emulator's check; op lists that break them —
+    a SUM the next op does not reduce, a FROM_SUM with no SUM before it, SUM on a direct
+    (3-tap) conv or with a second output, SUM in a multi-pair stage — are rejected by
+    both, so a misuse of the public ABI raises instead of reading stale partial sums."""
+    import copy
+    import ctypes
+    from cnn_gp import _native as N
+    lib = N.load()
+
+    def lib_ok(st):
+        arr = net._ops_array(st, None)
+        return lib.cgp_net_validate(ctypes.byref(arr), st.n_ops, st.pairs) == 0
+
+    def emu_ok(st):
+        try:
+            E.validate(st)
+            return True
+        except ValueError:
+            return False
+
+    for cfg in ("mnist_paper_convnet_gp", "mnist_paper_residual_cnn_gp", "mnist_as_tf",
+                "cifar10"):
+        C, side = specs.GEOMETRY[cfg]
+        net = NetPlan(Plan(configs_util.model(cfg), side, side))
+        for st in net.stages:
+            assert lib_ok(st) and emu_ok(st), cfg
+    net = NetPlan(Plan(configs_util.model("mnist_paper_convnet_gp"), 28, 28))
+    st = net.stages[0]
+    recs = [f for f, _ in st.records]
+    k = next(i for i, f in enumerate(recs) if f["kind"] == 0 and f["code"] & N.CGP_NET_CODE_SUM)
+
+    def broken(edit):
+        b = copy.deepcopy(st)
+        edit([f for f, _ in b.records])
+        return b
+
+    cases = [
+        lambda r: r[k + 1].__setitem__("code", r[k + 1]["code"] & ~N.CGP_NET_CODE_FROM_SUM),
+        lambda r: r[k].__setitem__("code", r[k]["code"] & ~N.CGP_NET_CODE_SUM),
+        lambda r: r[k].__setitem__("dst2", r[k]["src"]),
+        lambda r: r[k + 1].__setitem__("src", r[k + 1]["src"] + 1),
+    ]
+    for edit in cases:
+        b = broken(edit)
+        assert not lib_ok(b) and not emu_ok(b)
+    # SUM on a direct 3x3 conv (mnist_as_tf's) and SUM in a 4-pair stage
+    tf = NetPlan(Plan(configs_util.model("mnist_as_tf"), 28, 28))
+    d = copy.deepcopy(tf.stages[0])
+    r = [f for f, _ in d.records]
+    j = next(i for i, f in enumerate(r) if f["kind"] == 0 and f["geom"][4] == 3)
+    r[j]["code"] |= N.CGP_NET_CODE_SUM
+    assert not lib_ok(d) and not emu_ok(d)
+    m = copy.deepcopy(st)
+    m.pairs = 4
+    assert not lib_ok(m) and not emu_ok(m)

@@ -19,15 +19,42 @@ from conftest import PKG
 HDR = os.path.join(PKG, "csrc", "relu_poly.h")
 
 
-def coeffs(kind):
+def default_degree():
+    """The double degree on [0, 1/2] the default build compiles: CGP_RELU_TOL (default 1)
+    picks the first CGP_RELU_DEG_D default (the 1e-12 tables), else the second."""
+    txt = open(HDR).read()
+    tol = int(re.search(r"#define CGP_RELU_TOL (\d+)", txt).group(1))
+    degs = [int(d) for d in re.findall(r"#define CGP_RELU_DEG_D (\d+)", txt)]
+    return degs[0] if tol else degs[1]
+
+
+# max relative error of the default double polynomial (relu_poly.h: degree 11, 7.6e-13;
+# degree 13 with CGP_RELU_TOL=0, 1.6e-14)
+BOUND_D = {11: 7.7e-13, 13: 1.6e-14}
+
+
+def coeffs(kind, deg=None):
     """The coefficient table the default build compiles (the double one is selected by
-    CGP_RELU_DEG_D among several degrees)."""
+    CGP_RELU_DEG_D among several degrees; ``deg`` picks another)."""
     txt = open(HDR).read()
     n = r"\d+"
     if kind == "D":
-        n = str(int(re.search(r"#define CGP_RELU_DEG_D (\d+)", txt).group(1)) + 1)
+        n = str((deg or default_degree()) + 1)
     body = re.search(r"kReluPoly%s\[%s\] = \{(.*?)\};" % (kind, n), txt, re.S).group(1)
     return [float(v.strip().rstrip("f")) for v in body.split(",") if v.strip()]
+
+
+def adapt_tables(tol):
+    """(xmax, coefficients) of the range-adaptive fits in the CGP_RELU_TOL = tol branch"""
+    txt = open(HDR).read()
+    a = txt.index("#if CGP_RELU_TOL\n// x in")
+    b = txt.index("#else", a)
+    c = txt.index("#endif", b)
+    blk = txt[a:b] if tol else txt[b:c]
+    xs = [float(v) for v in re.findall(r"kReluAdaptX\d = ([0-9.]+);", blk)]
+    ps = [[float(v) for v in body.split(",") if v.strip()]
+          for body in re.findall(r"kReluAdaptP\d\[\d+\] = \{(.*?)\};", blk, re.S)]
+    return list(zip(xs, ps))
 
 
 def closed_form(c, v1, v2, cf, dt=np.float64):
@@ -81,7 +108,8 @@ def test_closed_form_matches_reference_formula():
     err = np.abs(got - ref) / scale
     # away from |rho| = 1 both are accurate to a few ulps of sqrt(t)
     mid = np.abs(rho) < 0.999
-    assert err[mid].max() < 1e-14, err[mid].max()
+    # (the polynomial's own bound plus a few ulps: degree 13 gave 1e-14)
+    assert err[mid].max() < max(1e-14, BOUND_D[default_degree()]), err[mid].max()
     # near |rho| = 1 the reference's acos(rho) carries ~sqrt(eps) noise
     assert err.max() < 3e-8, err.max()
 
@@ -90,9 +118,10 @@ def test_closed_form_known_answers():
     cf = coeffs("D")
     s6 = np.sqrt(6.0)
     got = closed_form([0.0, s6, -s6, 0.0], [2.0, 2.0, 2.0, 0.0], [3.0, 3.0, 3.0, 0.0], cf)
-    # rho = 0 is the end x = 1/2 of the fit, where the degree-13 polynomial is furthest
-    # off: 1.5e-14 relative (relu_poly.h)
-    assert abs(got[0] - s6 / (2 * np.pi)) < 2e-14 * s6 / (2 * np.pi)
+    # rho = 0 is the end x = 1/2 of the fit, where the polynomial is furthest off
+    # (relu_poly.h: 1.5e-14 relative at degree 13, 7.6e-13 at the default 11)
+    bound = max(2e-14, BOUND_D[default_degree()])
+    assert abs(got[0] - s6 / (2 * np.pi)) < bound * s6 / (2 * np.pi)
     assert abs(got[1] - s6 / 2) < 1e-15          # exact here (the reference: 4e-9 off)
     assert abs(got[2]) < 1e-15
     assert abs(got[3] - 1.7255613506e-20) / 1.7255613506e-20 < 1e-9
@@ -107,7 +136,8 @@ def test_closed_form_against_50_digit_map():
         c = rho * np.sqrt(v1 * v2)
         got = closed_form([c], [v1], [v2], cf)[0]
         ref = exact_dec(c, v1, v2)
-        assert abs(got - ref) <= 4e-15 * np.sqrt(v1 * v2), (rho, got, ref)
+        assert abs(got - ref) <= max(4e-15, BOUND_D[default_degree()]) * np.sqrt(v1 * v2), \
+            (rho, got, ref)
 
 
 def test_float_closed_form():
@@ -149,7 +179,7 @@ def test_chain_tables_hold_each_degree_at_the_degree13_bound():
     d0, xs, rows = chain_tables()
     assert len(rows) == 14 - d0 and all(len(r) == 14 for r in rows)
     assert xs == sorted(xs) and len(xs) == len(rows) - 1
-    full = coeffs("D")
+    full = coeffs("D", 13)
     assert rows[-1][0] == full[13] and rows[-1][1:] == full[12::-1]
     getcontext().prec = 50
     sys.path.insert(0, os.path.join(os.path.dirname(PKG), "tools"))
@@ -163,3 +193,23 @@ def test_chain_tables_hold_each_degree_at_the_degree13_bound():
         got = chain_eval(row, d, x)
         ref = np.array([float(P_dec(Decimal(float(v)))) for v in x])
         assert np.max(np.abs(got - ref) / ref) < 1.6e-14, (d, np.max(np.abs(got - ref) / ref))
+
+
+def test_adaptive_tables_hold_their_bounds():
+    """The range-adaptive sub-interval fits (relu_q_n's votes): the default CGP_RELU_TOL=1
+    tables (degrees 6 / 8 / 9 on [0, 1/8] / [0, 1/4] / [0, 3/8]) within 1e-12 of the exact
+    P, the CGP_RELU_TOL=0 ones (7 / 9 / 11) within 1e-14"""
+    getcontext().prec = 50
+    sys.path.insert(0, os.path.join(os.path.dirname(PKG), "tools"))
+    from fit_relu_poly import P_dec
+    for tol, bound, degs in ((1, 1e-12, [6, 8, 9]), (0, 1e-14, [7, 9, 11])):
+        tabs = adapt_tables(tol)
+        assert [len(p) - 1 for _, p in tabs] == degs
+        assert [x for x, _ in tabs] == [0.125, 0.25, 0.375]
+        for xmax, p in tabs:
+            x = np.linspace(0.0, xmax, 129)
+            got = np.full_like(x, p[-1])
+            for k in reversed(p[:-1]):
+                got = got * x + k
+            ref = np.array([float(P_dec(Decimal(float(v)))) for v in x])
+            assert np.max(np.abs(got - ref) / ref) < bound, (tol, xmax)

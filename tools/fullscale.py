@@ -133,23 +133,24 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
     kxx_bytes = n * n * 8
     res.update({k: out[k] for k in ("kxx_s", "gather_kxx_s", "kxx_to_kxz_s", "predict_s",
                                     "total_s")})
-    ph = saved["phases"]
+    ph = saved.get("phases")
     res.update(solve_s=out["solve_s"], kxz_s_rank0=out["kxz_s_rank"],
                solve_tflops=round(n ** 3 / 3 / out["solve_s"] / 1e12, 2),
-               harness_s=round(saved["rows_s"], 4),
-               solve_split={"widen_s": out.get("widen_s", 0.0),
-                            "jitter_s": round(ph["jitter_s"], 4),
-                            "factor_s": round(ph["factor_s"], 4),
-                            "potrs_s": round(ph["potrs_s"], 4),
-                            "rest_s": round(out["solve_s"] - out.get("widen_s", 0.0) -
-                                            sum(ph.values()), 4),
-                            "factor_tflops": round(n ** 3 / 3 / ph["factor_s"] / 1e12, 2),
-                            "note": "solve_s = widen (float32 K only) + jitter + Cholesky + "
-                                    "dpotrs (HIP events inside cgp_chol_solve_f64) + rest "
-                                    "(Y/alpha transposes, host); harness_s = the 8 residual "
-                                    "rows copied before K is factored in place (outside "
-                                    "solve_s, inside total_s)"},
-               kxx_pairs_per_s=round(n * (n - 1) / 2 / out["kxx_s"], 1),
+               harness_s=round(saved["rows_s"], 4))
+    if ph is not None:              # the solve's own HIP-event phases (solve.solve_phases)
+        res["solve_split"] = {"widen_s": out.get("widen_s", 0.0),
+                              "jitter_s": round(ph["jitter_s"], 4),
+                              "factor_s": round(ph["factor_s"], 4),
+                              "potrs_s": round(ph["potrs_s"], 4),
+                              "rest_s": round(out["solve_s"] - out.get("widen_s", 0.0) -
+                                              sum(ph.values()), 4),
+                              "factor_tflops": round(n ** 3 / 3 / ph["factor_s"] / 1e12, 2),
+                              "note": "solve_s = widen (float32 K only) + jitter + Cholesky "
+                                      "+ dpotrs (HIP events inside the solve) + rest (Y/alpha "
+                                      "transposes, host); harness_s = the 8 residual rows "
+                                      "copied before K is factored in place (outside "
+                                      "solve_s, inside total_s)"}
+    res.update(kxx_pairs_per_s=round(n * (n - 1) / 2 / out["kxx_s"], 1),
                plan_kxx=out["plan_kxx"], plan_kxz=out["plan_kxz"],
                kxz_share=out["kxz_share"],
                rank0_peak_gb_kxx_build=round(out["peak_bytes_kxx_build"] / 1e9, 2),
