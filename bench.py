@@ -1053,7 +1053,7 @@ def main(argv=None):
             max(2, args.steps // 4), cpu_ok), est_s=40))
 
     # --- the literal drop-in path (save_kernel.py's loop), beside the bound build ---
-    if rank == 0 and not args.no_dropin:
+    if world == 1 and not args.no_dropin:       # a per-process path: measured at N = 1
         put("dropin", legs.run("dropin", lambda: dropin_leg(
             (args.config, "mnist_as_tf"), args.dropin_n, (200, 1024), dev),
             multi_rank=False, est_s=20))

@@ -71,18 +71,22 @@ for s in "${LIST[@]}"; do
         line "$O/failleg.log" ;;
     tile4096)
         step tile4096 900 python bench.py --tile 4096 --steps 2 --warmup 1 --no-cpu \
-            --no-f32 --no-fullscale --no-fullscale-cifar10 --no-second --no-cifar10
+            --no-f32 --no-fullscale --no-fullscale-cifar10 --no-second --no-cifar10 --no-dropin
         line "$O/tile4096.log" ;;
     trace:*)
         cfg=${s#trace:}
         step "trace_$cfg" 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/trace_$cfg" \
             -o trace -- python bench.py --config "$cfg" --steps 3 --no-cpu --no-fullscale \
-            --no-fullscale-cifar10 --no-second --no-cifar10 --no-f32
+            --no-fullscale-cifar10 --no-second --no-cifar10 --no-f32 --no-dropin
         line "$O/trace_$cfg.log" ;;
     pmc)
         OUT=$O/pmc bash tools/pmc.sh > "$O/pmc.log" 2>&1 || { tail -n 30 "$O/pmc.log"; exit 1; }
         python3 tools/pmc_r2.py "$O/pmc" "$O/net_pmc.json" > /dev/null || exit 1
         echo "== pmc -> $O/net_pmc.json" ;;
+    pmc_ta)
+        PMC_CFGS="${PMC_CFGS:-mnist_paper_convnet_gp mnist_as_tf cifar10}" OUT=$O/pmc_ta \
+            bash tools/pmc_ta.sh > "$O/pmc_ta.log" 2>&1 || { tail -n 30 "$O/pmc_ta.log"; exit 1; }
+        tail -n 5 "$O/pmc_ta.log" ;;
     fullscale)
         step fullscale 900 python tools/fullscale.py ${FS_ARGS:-}
         tail -n 1 "$O/fullscale.log" ;;
