@@ -140,16 +140,25 @@ class DiagIterator:
 
     def __init__(self, batch_size, X, X2=None):
         self.batch_size = batch_size
-        dl = DataLoader(X, batch_size=batch_size)
+        dl = self._batches(X, batch_size)
         if X2 is None:
             self.same = True
             self.it = iter(enumerate(dl))
             self.length = len(dl)
         else:
-            dl2 = DataLoader(X2, batch_size=batch_size)
+            dl2 = self._batches(X2, batch_size)
             self.same = False
             self.it = iter(enumerate(zip(dl, dl2)))
             self.length = min(len(dl), len(dl2))
+
+    @staticmethod
+    def _batches(X, batch_size):
+        """The DataLoader's batches of X — sliced from the backing tensors when X is a
+        TensorDataset / Subset / ConcatDataset of them (tensor_rows), else the DataLoader"""
+        n = len(X)
+        if tensor_rows(X, 0, min(n, 1)) is None:
+            return DataLoader(X, batch_size=batch_size)
+        return [tensor_rows(X, lo, min(lo + batch_size, n)) for lo in range(0, n, batch_size)]
 
     def __iter__(self):
         return self

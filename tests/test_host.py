@@ -480,3 +480,22 @@ def test_op_record_template_equals_records_built_per_call(name, dt):
         ref = net._ops_array(st, var, states[sidx], states[sidx + 1])
         assert bytes(buf) == bytes(ref)
         assert program == ids[sidx]
+
+
+def test_diag_iterator_batches_equal_dataloader():
+    from torch.utils.data import ConcatDataset, DataLoader, Subset, TensorDataset
+    from cnn_gp.data import DiagIterator
+    g = torch.Generator().manual_seed(1)
+    a = TensorDataset(torch.rand((37, 1, 3, 3), generator=g), torch.arange(37))
+    b = TensorDataset(torch.rand((20, 1, 3, 3), generator=g), torch.arange(20))
+    X = Subset(ConcatDataset([a, b]), range(10, 50))
+    Y = Subset(ConcatDataset([a, b]), range(0, 40))
+    for X2 in (None, Y):
+        got = list(DiagIterator(16, X, X2))
+        ref = list(zip(DataLoader(X, batch_size=16), DataLoader(X2 if X2 is not None else X,
+                                                                batch_size=16)))
+        assert len(got) == len(ref) == 3
+        for (same, (i, xy), (j, xy2)), (rx, ry) in zip(got, ref):
+            assert same == (X2 is None) and i == j
+            assert torch.equal(xy[0], rx[0]) and torch.equal(xy2[0], ry[0])
+            assert torch.equal(xy[1], rx[1])
