@@ -738,26 +738,33 @@ class NetPlan:
                 quarters.append((vx, q))
                 keep.append(q)
                 var[v] = (q, vy)
-        for sidx, st in enumerate(self.stages):
-            tmpl, slots, what, program = self._ops_template(sidx, st, flags, x.element_size())
+        # every stage's op records in one pinned buffer and one H2D copy.  Pinned +
+        # non_blocking: a pageable H2D copy would block the host until the previous tile's
+        # kernels drained, leaving the GPU idle while this tile's small launches are issued;
+        # the caching host allocator keeps the pinned block until the copy has run
+        tmpls = [self._ops_template(sidx, st, flags, x.element_size())
+                 for sidx, st in enumerate(self.stages)]
+        offs = [0]
+        for t in tmpls:
+            offs.append(offs[-1] + len(t[0]))
+        host = torch.empty((offs[-1],), dtype=torch.uint8, pin_memory=True)
+        hb = host.numpy()
+        for sidx, (tmpl, slots, what, _) in enumerate(tmpls):
             ptrs = [var[w[0]][w[1]].data_ptr() if isinstance(w, tuple) else
                     (states[sidx] if w == "in" else states[sidx + 1]).data_ptr()
                     for w in what]
-            # pinned + non_blocking: a pageable H2D copy would block the host until the
-            # previous tile's kernels drained, leaving the GPU idle while this tile's small
-            # launches are issued; the caching host allocator keeps the pinned block until
-            # the copy has run
-            host = torch.empty((len(tmpl),), dtype=torch.uint8, pin_memory=True)
-            hb = host.numpy()
-            hb[:] = tmpl
-            hb.view("<u8")[slots] = ptrs
-            ops_dev = host.to(x.device, non_blocking=True)   # stream-ordered, freed stream-ordered
-            keep.append(ops_dev)
+            blk = hb[offs[sidx]:offs[sidx + 1]]
+            blk[:] = tmpl
+            blk.view("<u8")[slots] = ptrs
+        ops_dev = host.to(x.device, non_blocking=True)   # stream-ordered, freed stream-ordered
+        keep.append(ops_dev)
+        for sidx, st in enumerate(self.stages):
+            program = tmpls[sidx][3]
             a = N.NetArgs()
             a.x, a.y, a.out = x.data_ptr(), y.data_ptr(), out.data_ptr()
             if same:
                 a.kdiag = var[self.plan.vf][0].data_ptr()
-            a.ops = ops_dev.data_ptr()
+            a.ops = ops_dev.data_ptr() + offs[sidx]    # records are 8-byte aligned
             a.n1, a.n2, a.ldo = n1, n2, out.stride(0)
             a.nops, a.channels, a.h, a.w = st.n_ops, x.shape[1], x.shape[2], x.shape[3]
             a.same, a.final_slot, a.hs, a.lds_elems = int(same), st.final_slot, 0, st.lds_elems
