@@ -74,10 +74,6 @@ namespace {
 
 constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kChunkElems = 2048;    // map elements one workgroup stages per chunk
-#ifndef CGP_GEO_STAGE_OUT
-#define CGP_GEO_STAGE_OUT 0
-#endif
-constexpr bool kGeoStageOut = CGP_GEO_STAGE_OUT != 0;
 constexpr int kEMax = kChunkElems / kBlock;   // prefetch registers per thread (8)
 constexpr int kMaxLds = 64 * 1024;   // bytes of LDS one conv workgroup may take
 
@@ -373,7 +369,6 @@ struct GeoP {
     long long nmaps, nchunks;
     FastDiv n2;
     int channels, pre, post, add, same, diag;
-    int stage_out;   // outputs through LDS, 16-byte stores (CGP_GEO_STAGE_OUT, A/B)
     T weight, bias;
 };
 
@@ -519,7 +514,6 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
 
         // ---- stage 3: column sums over R3 rows per item, epilogue, store ----
         T* out = p.out + m0 * G::HOWO;
-        T* stg = reinterpret_cast<T*>(inbuf(buf));   // consumed in stage 1 (stage_out)
 #pragma unroll
         for (int k = 0; k < L::I3; ++k) {
             const int e = tid + k * kBlock;
@@ -555,29 +549,10 @@ __global__ __launch_bounds__(kBlock) void conv_geo_kernel(const GeoP<T> p) {
 #pragma unroll
                 for (int o = 0; o < G::R3; ++o) {
                     // (non-temporal stores measured -5%: profiles/r4/ab_r4f_stencil_nt_store.log)
-                    if (oh0 + o < G::HO) {
-                        const unsigned q = (unsigned)(ml * G::HOWO + (oh0 + o) * G::WO + ow);
-                        if (p.stage_out)
-                            stg[q] = res[o];
-                        else
-                            out[q] = res[o];
-                    }
+                    if (oh0 + o < G::HO)
+                        out[(unsigned)(ml * G::HOWO + (oh0 + o) * G::WO + ow)] = res[o];
                 }
             }
-        }
-        if (p.stage_out) {
-            // the chunk's outputs are one contiguous run of mb·HO·WO elements: staged in the
-            // input buffer stage 1 has consumed (its next DMA is issued below, after a
-            // barrier) and written 16 bytes per lane, instead of the column items' 8-byte
-            // stores in 224-byte row segments
-            lds_barrier();
-            constexpr int V = 16 / (int)sizeof(T);
-            typedef T vec_t __attribute__((ext_vector_type(V)));
-            const int nv = mb * G::HOWO / V;
-            const vec_t* sv = reinterpret_cast<const vec_t*>(stg);
-            vec_t* dv = reinterpret_cast<vec_t*>(out);
-            for (int v = tid; v < nv; v += kBlock) dv[v] = sv[v];
-            lds_barrier();
         }
         // buffer `buf` was consumed in stage 1: fetch chunk k+2 into it (unconditional —
         // past the end it re-fetches this chunk — so every path issues exactly PW ops)
@@ -1082,11 +1057,6 @@ int launch_geo(const cgp_conv_args* a, hipStream_t s) {
     p.diag = a->diag;
     p.weight = (T)a->weight;
     p.bias = (T)a->bias;
-    // every chunk's output run starts 16-byte aligned (HO·WO·sizeof(T) a multiple of 16)
-    // and fits the plane buffer it is staged in
-    p.stage_out = kGeoStageOut && (G::HOWO * sizeof(T)) % 16 == 0 &&
-                  L::MB * G::HOWO <= L::IN_STRIDE && ((uintptr_t)a->out % 16) == 0 &&
-                  a->pre != CGP_PRE_MOMENTS;
     const size_t lds = (size_t)L::ELEMS * sizeof(T);
     auto kern = conv_geo_kernel<T, G, PRE, POST, ADD>;
     int per_cu = 0;
