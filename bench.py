@@ -81,7 +81,7 @@ SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
 CLOCK_HZ = 2.4e9               # peak engine clock
 # committed PMC passes, newest first (a config missing from a newer file is looked up in
 # the older one)
-PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r4", "r3")]
+PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r5", "r4", "r3")]
 CALIB_FILES = [os.path.join(ROOT, "profiles", r, "cpu_calibration.json") for r in ("r4", "r2")]
 DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "120"))
 
@@ -733,7 +733,7 @@ def dropin_leg(cfg_names, n, tiles, dev):
     compared on the upper tiles.  pairs = N(N−1)/2 for both (the headline's count)."""
     import contextlib
     import numpy as np
-    from torch.utils.data import Subset, TensorDataset
+    from torch.utils.data import TensorDataset
     from cnn_gp.kernel_save_tools import save_K
     pairs = n * (n - 1) // 2
     out = {}
@@ -754,7 +754,8 @@ def dropin_leg(cfg_names, n, tiles, dev):
         mk = model_kern(model)
         for B in tiles:
             with contextlib.redirect_stdout(sys.stderr):   # save_K's progress lines
-                save_K(MemH5(), kern, "Kxx", Subset(ds, range(min(n, 2 * B))), None, False, B)
+                # warm: one whole pass (every tile shape, the ragged edge's included)
+                save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9)
                 torch.cuda.synchronize()
                 f = MemH5()
                 t0 = time.perf_counter()
