@@ -45,8 +45,9 @@ def main(path):
             print(f"  {k}", {x: f.get(x) for x in keys if x in f})
             if f.get("solve_split"):
                 print("    split", {x: v for x, v in f["solve_split"].items() if x != "note"})
-            for rk in f.get("ranks") or []:
-                print("    rank", rk)
+            rk = f.get("ranks")
+            if rk:
+                print("    ranks", rk)
     di = d.get("dropin")
     if di:
         print("  dropin", di)
@@ -54,7 +55,7 @@ def main(path):
         print("  WATCHDOG", d["watchdog"])
     f32 = d.get("f32")
     if f32:
-        print("  f32", {k: (v.get("value") if isinstance(v, dict) else None)
+        print("  f32", {k: (v.get("value") if isinstance(v, dict) else v)
                         for k, v in f32.items() if k != "note"})
     cpu = d.get("cpu_baseline")
     if cpu:
