@@ -47,7 +47,7 @@ def coeffs(kind, deg=None):
 def adapt_tables(tol):
     """(xmax, coefficients) of the range-adaptive fits in the CGP_RELU_TOL = tol branch"""
     txt = open(HDR).read()
-    a = txt.index("#elif CGP_RELU_TOL\n// x in")
+    a = txt.index("#if CGP_RELU_TOL\n// x in")
     b = txt.index("#else", a)
     c = txt.index("#endif", b)
     blk = txt[a:b] if tol else txt[b:c]

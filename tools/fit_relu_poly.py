@@ -122,9 +122,6 @@ ADAPT = ((0.125, 7), (0.25, 9), (0.375, 11))
 # 2.2e-13 / 1.3e-13 / 9.2e-13 / 7.6e-13), 3-5 decades inside the end-to-end parity bounds
 #  and 4 inside the reference's own acos noise near |rho| = 1
 ADAPT_TOL = ((0.125, 6), (0.25, 8), (0.375, 9))
-# CGP_RELU_TOL=2 (A/B): the same degrees on the widest intervals within the bound
-# (8.6e-13 / 8.8e-13 / 9.2e-13)
-ADAPT_TOL2 = ((0.15, 6), (0.3, 8), (0.375, 9))
 DEG_TOL = 11
 # ... and for the float polynomial (its bound: the degree-6 fit's 7.9e-8)
 ADAPT_F = ((0.125, 3), (0.375, 5))
@@ -148,8 +145,6 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
            for xm, d in ADAPT]
     sub_tol = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
                for xm, d in ADAPT_TOL]
-    sub_tol2 = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
-                for xm, d in ADAPT_TOL2]
     sub_f = [(xm, d, check(to_x(fit(d, xm), xm), np.float32, npts=4001, xmax=xm))
              for xm, d in ADAPT_F]
     chain = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
@@ -184,8 +179,7 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
         lines += [f"    {float(c)!r}," for c in dbl[d][1]]
         lines += ["};"]
     lines += ["#else", "#error \"CGP_RELU_DEG_D: no table for this degree\"", "#endif"]
-    for tag, rows in (("#if CGP_RELU_TOL == 2", sub_tol2), ("#elif CGP_RELU_TOL", sub_tol),
-                      ("#else", sub)):
+    for tag, rows in (("#if CGP_RELU_TOL", sub_tol), ("#else", sub)):
         lines += [tag]
         for k, (xm, d, (err, cfs)) in enumerate(rows):
             lines += [f"// x in [0, {xm}]: degree {d}, max rel err {err:.2e}",
