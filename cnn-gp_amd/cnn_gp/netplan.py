@@ -55,6 +55,8 @@ FUSE_REDUCE = os.environ.get("CGP_NET_FUSE_REDUCE", "1") != "0"
 # library builds that predate it (tools/variants.sh)
 QUARTER_MAPS = os.environ.get("CGP_NET_QUARTER", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
+# state buffers below this size are allocated without asking for the free memory
+SMALL_STATE_BYTES = 512 << 20
 
 
 class Unsupported(Exception):
@@ -683,9 +685,12 @@ class NetPlan:
         most STATE_FREE_FRAC of the device's free memory; a multiple of 64, at least 64."""
         stride = max(max(st.load_stride, st.store_stride) for st in self.stages)
         chunk = CHUNK_BYTES // (stride * itemsize)
-        if device is not None and torch.device(device).type == "cuda":
+        per_unit = sum(st.load_stride for st in self.stages[1:]) * itemsize
+        # the free-memory query (hipMemGetInfo: 0.1-0.5 ms, a B = 200 tile's kernel time)
+        # only when the state buffers could be large; below SMALL_STATE_BYTES they fit
+        if device is not None and torch.device(device).type == "cuda" and \
+                min(chunk, units) * per_unit > SMALL_STATE_BYTES:
             free = torch.cuda.mem_get_info(device)[0]
-            per_unit = sum(st.load_stride for st in self.stages[1:]) * itemsize
             chunk = min(chunk, int(free * STATE_FREE_FRAC) // max(1, per_unit))
         return min(max(64, chunk // 64 * 64), units)
 
@@ -822,11 +827,14 @@ class NetPlan:
         """Values whose x-side variance maps the fp64 closed-form ReLU reads quartered."""
         if dtype != torch.float64 or flags & N.CGP_FLAG_EXACT_RELU or not QUARTER_MAPS:
             return set()
-        used = set()
-        for st in self.stages:
-            used |= {v for _, v in st.records if v is not None}
-            used |= {f["var2"] for f, _ in st.records if "var2" in f}
-        return used
+        used = self.__dict__.get("_quarter_used")
+        if used is None:                 # asked on every forward: the walk once per plan
+            used = set()
+            for st in self.stages:
+                used |= {v for _, v in st.records if v is not None}
+                used |= {f["var2"] for f, _ in st.records if "var2" in f}
+            self.__dict__["_quarter_used"] = used
+        return set(used)
 
     def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
             out: Optional[torch.Tensor] = None, qvar: Optional[dict] = None):
