@@ -873,6 +873,8 @@ def compact_line(full: dict) -> dict:
     for k in ("error", "watchdog"):
         if full.get(k) is not None:
             line[k] = str(full[k])[:300]
+    if full.get("elapsed_s") is not None:
+        line["elapsed_s"] = full["elapsed_s"]          # the whole run, rank 0's clock
     line["roofline"] = _pick(full.get("roofline"), _ROOF_KEYS)
     line["cpu_baseline"] = _cpu(full.get("cpu_baseline"))
     line["reference_schedule_pairs_per_s"] = _sig(full.get("reference_schedule_pairs_per_s"))
@@ -961,6 +963,7 @@ def main(argv=None):
 
     def make_line(watchdog=False):
         snap = dict(full)
+        snap["elapsed_s"] = round(deadline.elapsed(), 1)
         if watchdog:
             snap["watchdog"] = (f"hard limit {deadline.hard_s:.0f} s reached during leg "
                                 f"{legs.current!r}; later legs not run")
