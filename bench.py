@@ -82,6 +82,8 @@ CLOCK_HZ = 2.4e9               # peak engine clock
 # committed PMC passes, newest first (a config missing from a newer file is looked up in
 # the older one)
 PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r5", "r4", "r3")]
+# the fp64 flop counters of the same kernel code (tools/pmc_flops.sh)
+FLOPS_FILES = [os.path.join(ROOT, "profiles", r, "flops_pmc.json") for r in ("r5",)]
 CALIB_FILES = [os.path.join(ROOT, "profiles", r, "cpu_calibration.json") for r in ("r4", "r2")]
 DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "120"))
 
@@ -483,10 +485,20 @@ def net_roofline(model, x, cfg_name, timing):
         valu_insts = round(pmc["valu_insts_per_pair"], 1)
         pmc_note = (f"PMC ({pmc_file}): {pmc['source']}; per pair: {pmc['hbm_bytes_per_pair']:.0f} HBM "
                     f"bytes, {pmc['valu_insts_per_pair']:.0f} VALU wave-instructions")
+    # issued fp64 flops: every lane of every issued fp64 instruction (PMC flop counters of
+    # the same code, per pair) over this run's live launch time — what the kernel executes,
+    # where `achieved` credits the reference's direct-stencil flops
+    issued = issued_frac = None
+    fpmc, _ = committed(FLOPS_FILES, cfg_name)
+    if fpmc and x.dtype == torch.float64:
+        issued = fpmc["issued_lane_flops_per_pair"] * pairs / (ms * 1e-3) / 1e12
+        issued_frac = round(issued / FP64_PEAK_TFLOPS, 4)
+        issued = round(issued, 2)
     kname = f"net_kernel<{'double' if x.dtype == torch.float64 else 'float'}>"
     return {"bound": "valu_f64", "achieved": round(achieved, 2), "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
             "traffic": traffic, "valu_issue_frac": valu,
+            "issued_fp64_tflops": issued, "issued_fp64_frac": issued_frac,
             "kernel": kname, "launches": len(timing), "avg_ms": round(ms / len(timing), 4),
             "pairs_per_launch": int(per_launch), "alg_flops_per_pair": fl,
             "alg_flops_per_launch": int(fl * per_launch),
@@ -811,7 +823,7 @@ def _pick(d, keys, digits=4):
 
 
 _ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "avg_ms",
-              "valu_issue_frac", "valu_insts_per_pair", "launches")
+              "valu_issue_frac", "issued_fp64_frac", "valu_insts_per_pair", "launches")
 _CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "reference_equivalent_pairs_per_s")
 _FS_KEYS = ("n", "m", "total_s", "kxx_s", "kxx_pairs_per_s", "kxz_s", "kxz_s_rank0",
             "gather_kxx_s", "solve_s", "solve_tflops", "predict_s", "residual",

@@ -83,6 +83,10 @@ for s in "${LIST[@]}"; do
         OUT=$O/pmc bash tools/pmc.sh > "$O/pmc.log" 2>&1 || { tail -n 30 "$O/pmc.log"; exit 1; }
         python3 tools/pmc_r2.py "$O/pmc" "$O/net_pmc.json" > /dev/null || exit 1
         echo "== pmc -> $O/net_pmc.json" ;;
+    pmc_flops)
+        OUT=$O/pmc_flops bash tools/pmc_flops.sh > "$O/pmc_flops.log" 2>&1 || \
+            { tail -n 30 "$O/pmc_flops.log"; exit 1; }
+        grep -E "executed_flops_per_pair|lane_fill|executed_tflops" "$O/pmc_flops.log" ;;
     pmc_ta)
         PMC_CFGS="${PMC_CFGS:-mnist_paper_convnet_gp mnist_as_tf cifar10}" OUT=$O/pmc_ta \
             bash tools/pmc_ta.sh > "$O/pmc_ta.log" 2>&1 || { tail -n 30 "$O/pmc_ta.log"; exit 1; }
