@@ -21,34 +21,38 @@ mirrors; K[i, i] comes from the per-image variance chain).  The reference's sche
 would count B² for a diagonal tile; that figure is reported as
 ``reference_schedule_pairs_per_s`` beside it.
 
-Also on the same JSON line (each in its own slot; a leg that fails records
-{"error": ...} there and the line still prints):
+Also on the same JSON line, in this order (each in its own slot; a leg that fails records
+{"error": ...} there and the line still prints; the line is compact_line() of the full
+result, which is written to gpurun_out/bench_full.json — DESIGN.md §6 defines each leg):
   roofline           the whole-network kernel (net_kernel, fp64 VALU-bound): credited
-                     direct-stencil flops vs the fp64 peak, plus the VALU issue
-                     utilisation and HBM traffic per launch from the committed PMC
-                     passes (profiles/r4/net_pmc.json, rocprofv3)
-  mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
-  cifar10            the same harness on configs[4]'s network (3×32×32, Kxx 4096²)
-  solve              rocSOLVER/rocBLAS blocked Cholesky + dpotrs_64 on the assembled Kxx
-  fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
-                     + solve + predict, row strips per rank, Kxx received into rank 0's
-                     matrix point-to-point, solve overlapped with the Kxz strips, only
-                     the scores gathered (tools/fullscale.py, cnn_gp/pipeline.py)
-  fullscale_cifar10  BASELINE configs[4]: cifar10 Kxx 50 000² + Kxz + solve + predict
+                     direct-stencil flops vs the fp64 peak, the issued fp64 flops and the
+                     VALU issue fraction and HBM traffic from the committed PMC passes
+  cpu_baseline       the torch-CPU restatement of the reference (oracle/torch_cpu.py,
+                     bit-identical to the reference at C1) on the host threads torch is
+                     given, with the committed calibration against the reference
   conv_stencil_roofline  Conv2d.propagate alone (the north star's "Conv2d covariance
                      kernel") against the 8 TB/s HBM roof, PMC traffic committed
-  cpu_baseline       the torch-CPU restatement of the reference (oracle/torch_cpu.py,
-                     bit-identical to the reference at C1) on the host threads torch
-                     is given, with the committed calibration against the reference
+  mnist_as_tf        the same harness on BASELINE configs[2] (ResNet-GP, 32 layers)
+  solve              the blocked Cholesky + dpotrs_64 on the assembled Kxx
+  cifar10            the same harness on configs[4]'s network (3×32×32, Kxx 4096²)
+  dropin             save_kernel.py's own loop (save_K + a per-tile kern, float32) at
+                     batch 200 and 1024 beside the bound build (one rank only)
+  f32                the Kxx legs with float32 kernels (the reference pipeline's precision)
+  fullscale          BASELINE configs[3]: mnist_as_tf Kxx 60 000² + Kxz 10 000 × 60 000
+                     + solve + predict (tools/fullscale.py, cnn_gp/pipeline.py)
+  fullscale_cifar10  BASELINE configs[4]: cifar10 Kxx 50 000² + Kxz + solve + predict
+  fullscale_f32      configs[3] with float32 kernels
 
 Multi-GPU (one process per GPU): the Kxx grows with the world (n_blocks² half-tile units
 >= world × the 1-GPU units, divisible by world) and its tiles are split over the ranks by
 evaluated pairs — no data-path collective; per-rank work is ~constant ("scaling":
 "weak").  The full-scale legs shard their fixed problems ("strong"): Kxx strips to rank 0
 point-to-point, α broadcast, scores gathered.  Every collective has a timeout
-(CGP_DIST_TIMEOUT_S, default 300 s) and raises instead of hanging; the legs' outcomes are
+(CGP_DIST_TIMEOUT_S, default 120 s) and raises instead of hanging; the legs' outcomes are
 exchanged over a gloo side group after each leg, so a failure on any rank is recorded
-and the remaining multi-rank legs are skipped.
+and the remaining multi-rank legs are skipped.  A leg that would start past
+CGP_BENCH_BUDGET_S (420 s) is skipped, and a watchdog prints the line at CGP_BENCH_HARD_S
+(540 s) whatever a rank is stuck in.
 """
 from __future__ import annotations
 
