@@ -159,3 +159,24 @@ def test_sum_contract_is_validated():
     m = copy.deepcopy(st)
     m.pairs = 4
     assert not lib_ok(m) and not emu_ok(m)
+
+
+def test_chunk_units_asks_free_memory_only_for_large_state(monkeypatch):
+    """the free-memory query (hipMemGetInfo, 0.1-0.5 ms) runs only when a launch group's
+    state buffers could exceed SMALL_STATE_BYTES: a per-tile forward at batch 200 never
+    asks, a full-scale B = 4096 tile does"""
+    from cnn_gp import netplan
+    calls = []
+
+    def fake_info(dev):
+        calls.append(dev)
+        return (64 << 30, 288 << 30)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", fake_info)
+    net = NetPlan(Plan(configs_util.model("mnist_as_tf"), 28, 28))
+    small = 40000                                 # a B = 200 Kxz tile: 25² supertiles · 64
+    assert net.chunk_units(8, small, "cuda:0") == small and not calls
+    big = 4096 * 4096
+    c = net.chunk_units(8, big, "cuda:0")
+    assert calls and 64 <= c < big and c % 64 == 0
+    per_unit = sum(st.load_stride for st in net.stages[1:]) * 8
+    assert c * per_unit <= (64 << 30) * netplan.STATE_FREE_FRAC
