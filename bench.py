@@ -894,6 +894,7 @@ def compact_line(full: dict) -> dict:
     line["roofline"] = _pick(full.get("roofline"), _ROOF_KEYS)
     line["cpu_baseline"] = _cpu(full.get("cpu_baseline"))
     line["reference_schedule_pairs_per_s"] = _sig(full.get("reference_schedule_pairs_per_s"))
+    line["unique_entries_per_s"] = _sig(full.get("unique_entries_per_s"))
     if "conv_stencil_roofline" in full:
         line["conv_stencil_roofline"] = _pick(
             full["conv_stencil_roofline"], ("bound", "achieved", "peak", "unit", "frac",
