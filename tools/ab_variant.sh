@@ -24,6 +24,6 @@ fi
 for data in rand mnist; do for rep in 1 2; do for v in cur $V; do
     lib=$PWD/cnn-gp_amd/lib/libcnngp.so; [ $v = $V ] && lib=$VL
     timeout -k 10 200 env CNNGP_LIB=$lib python tools/netbench.py --configs $CFGS --data $data \
-        > "$O/ab_${v}_${data}_$rep.log" 2>&1 || exit 1
+        ${NB_ARGS:-} > "$O/ab_${v}_${data}_$rep.log" 2>&1 || exit 1
     echo "-- $v $data $rep"; grep -v amdgpu.ids "$O/ab_${v}_${data}_$rep.log" | tail -n 3 | cut -c1-70
 done; done; done
