@@ -285,3 +285,41 @@ def test_watchdog_prints_the_line_when_a_rank_hangs():
             if p.is_alive():
                 p.kill()
             p.join(timeout=30)
+
+
+def _budget_worker(rank, world, port, q):
+    """rank 1 is past the budget, rank 0 is not: both skip the multi-rank leg (they agree
+    first, so no collective inside the leg pairs with nothing); rank-local legs follow each
+    rank's own clock"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = _bench()
+        d = b.Deadline(budget_s=100.0, hard_s=1000.0)
+        if rank == 1:
+            d.t0 -= 200.0
+        legs = b.Legs(world, rank, dist.new_group(backend="gloo"), d)
+        out = {"multi": legs.run("multi", lambda: "ran"),
+               "local": legs.run("local", lambda: "ran", multi_rank=False)}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_budget_skip_is_agreed():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_budget_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert "skipped: budget" in got[r]["multi"]["error"]
+    assert got[0]["local"] == "ran"
+    assert "skipped: budget" in got[1]["local"]["error"]
