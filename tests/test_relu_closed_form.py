@@ -153,48 +153,6 @@ def test_float_closed_form():
     assert err.max() < 2e-6, err.max()
 
 
-def chain_tables():
-    """relu_poly.h's per-degree tables (CGP_RELU_FINE / CGP_RELU_CHAIN): the lowest degree
-    d0, the thresholds of degrees d0..12 and the rows (degree d0 + r: a_d at [0], a_(13-j) at
-    [j] for the steps it runs)."""
-    txt = open(HDR).read()
-    d0 = int(re.search(r"kReluChainD0 = (\d+);", txt).group(1))
-    xs = re.search(r"kReluChainX\[\d+\] = \{(.*?)\};", txt, re.S).group(1)
-    body = re.search(r"kReluChainP\[\d+\]\[14\] = \{(.*?)\};", txt, re.S).group(1)
-    rows = [[float(v) for v in r.split(",") if v.strip()]
-            for r in re.findall(r"\{([^{}]*)\}", body)]
-    return d0, [float(v) for v in xs.split(",")], rows
-
-
-def chain_eval(row, d, x):
-    """horner_row / horner_chain (cgp_common.h) in numpy: p = a_d·x + t[14-d], then steps
-    15-d .. 13."""
-    p = row[0] * x + row[14 - d]
-    for j in range(15 - d, 14):
-        p = p * x + row[j]
-    return p
-
-
-def test_chain_tables_hold_each_degree_at_the_degree13_bound():
-    d0, xs, rows = chain_tables()
-    assert len(rows) == 14 - d0 and all(len(r) == 14 for r in rows)
-    assert xs == sorted(xs) and len(xs) == len(rows) - 1
-    full = coeffs("D", 13)
-    assert rows[-1][0] == full[13] and rows[-1][1:] == full[12::-1]
-    getcontext().prec = 50
-    sys.path.insert(0, os.path.join(os.path.dirname(PKG), "tools"))
-    from fit_relu_poly import P_dec
-    for r, row in enumerate(rows):
-        d = d0 + r
-        # the entries before the first step of degree d are unused zeros
-        assert all(v == 0.0 for v in row[1:14 - d]), d
-        xmax = xs[r] if r < len(xs) else 0.5
-        x = np.linspace(0.0, xmax, 257)
-        got = chain_eval(row, d, x)
-        ref = np.array([float(P_dec(Decimal(float(v)))) for v in x])
-        assert np.max(np.abs(got - ref) / ref) < 1.6e-14, (d, np.max(np.abs(got - ref) / ref))
-
-
 def test_adaptive_tables_hold_their_bounds():
     """The range-adaptive sub-interval fits (relu_q_n's votes): the default CGP_RELU_TOL=1
     tables (degrees 6 / 8 / 9 on [0, 1/8] / [0, 1/4] / [0, 3/8]) within 1e-12 of the exact

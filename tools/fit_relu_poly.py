@@ -125,11 +125,6 @@ ADAPT_TOL = ((0.125, 6), (0.25, 8), (0.375, 9))
 DEG_TOL = 11
 # ... and for the float polynomial (its bound: the degree-6 fit's 7.9e-8)
 ADAPT_F = ((0.125, 3), (0.375, 5))
-# every degree 6-12 on [0, xmax] at or below the degree-13 fit's bound, the degree-13
-# polynomial itself on [0, 1/2], in one table layout (kReluChainP): the fine-grained
-# adaptive ReLU (CGP_RELU_FINE) takes the wave's degree by a binary search of votes, and the
-# one-chain option (CGP_RELU_CHAIN) enters one unrolled degree-13 chain at that degree's step
-CHAIN = ((0.083, 6), (0.13, 7), (0.19, 8), (0.25, 9), (0.31, 10), (0.375, 11), (0.43, 12))
 
 
 def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
@@ -147,8 +142,6 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
                for xm, d in ADAPT_TOL]
     sub_f = [(xm, d, check(to_x(fit(d, xm), xm), np.float32, npts=4001, xmax=xm))
              for xm, d in ADAPT_F]
-    chain = [(xm, d, check(to_x(fit(d, xm), xm), np.float64, npts=4001, xmax=xm))
-             for xm, d in CHAIN]
     lines = [
         "// relu_poly.h - generated by tools/fit_relu_poly.py --write (do not edit by hand).",
         "// P(x), x = (1 - |rho|)/2 in [0, 1/2], monomials in x; the fast ReLU covariance map is",
@@ -196,22 +189,6 @@ def write_header(path, deg_d=13, deg_f=6, alt_d=(10, 11, 12)):
                   f"constexpr float kReluAdaptFP{k}[{d + 1}] = {{"]
         lines += [f"    {float(c)!r}f," for c in cfs]
         lines += ["};"]
-    # chain rows: degree CHAIN[0] + row; entry 0 = the top coefficient a_d, entry j = a_(13-j)
-    # for j >= 14 - d (the steps degree d runs), 0 before that
-    d0 = chain[0][1]
-    lines += [f"// per-degree tables (CGP_RELU_FINE, CGP_RELU_CHAIN): row r = degree {d0} + r on x in "
-              "[0, kReluChainX[r]]",
-              f"constexpr int kReluChainD0 = {d0};"]
-    lines += [f"//   degree {d}: x <= {xm}, max rel err {err:.2e}" for xm, d, (err, _) in chain]
-    lines += [f"//   degree {deg_d}: x <= 0.5, max rel err {dbl[deg_d][0]:.2e}"]
-    lines += [f"constexpr double kReluChainX[{len(chain)}] = {{"
-              + ", ".join(repr(xm) for xm, _, _ in chain) + "};",
-              f"constexpr double kReluChainP[{len(chain) + 1}][{deg_d + 1}] = {{"]
-    for xm, d, (err, cfs) in chain + [(0.5, deg_d, dbl[deg_d])]:
-        row = [float(cfs[d])] + [float(cfs[deg_d - j]) if j >= deg_d + 1 - d else 0.0
-                                 for j in range(1, deg_d + 1)]
-        lines += ["    {" + ", ".join(repr(v) for v in row) + "},"]
-    lines += ["};"]
     lines += [f"constexpr int kReluPolyDegF = {deg_f};",
               f"constexpr float kReluPolyF[{deg_f + 1}] = {{"]
     lines += [f"    {float(c)!r}f," for c in cf]
