@@ -50,10 +50,6 @@ USE_PROGRAMS = os.environ.get("CGP_NET_PROGRAMS", "1") != "0"
 # CGP_NET_CODE_FROM_SUM; one pair per workgroup or half): no map store, no map re-read,
 # one barrier less per pair.  CGP_NET_FUSE_REDUCE=0 keeps the two ops apart.
 FUSE_REDUCE = os.environ.get("CGP_NET_FUSE_REDUCE", "1") != "0"
-# scaled (cgp_net_xvar_scale() = 1/16) x-side variance maps for the fp64 closed-form ReLU
-# (relu_q_n; "quarter" names the round-2 1/4 scale); 0 only to time
-# library builds that predate it (tools/variants.sh)
-QUARTER_MAPS = os.environ.get("CGP_NET_QUARTER", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
 # state buffers below this size are allocated without asking for the free memory
 SMALL_STATE_BYTES = 512 << 20
@@ -825,7 +821,9 @@ class NetPlan:
 
     def quarter_vars(self, dtype, flags: int = 0) -> set:
         """Values whose x-side variance maps the fp64 closed-form ReLU reads quartered."""
-        if dtype != torch.float64 or flags & N.CGP_FLAG_EXACT_RELU or not QUARTER_MAPS:
+        # the fp64 closed-form ReLU (relu_q_n) reads its x-side maps scaled by
+        # cgp_net_xvar_scale() = 1/16 ("quarter": the round-2 name of the 1/4 scale)
+        if dtype != torch.float64 or flags & N.CGP_FLAG_EXACT_RELU:
             return set()
         used = self.__dict__.get("_quarter_used")
         if used is None:                 # asked on every forward: the walk once per plan

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an A/B variant of libcnngp: netfuse.hip (default), cnngp.hip (VARIANT_SRC=cnngp) or
 # both (VARIANT_SRC=both) compiled with extra -D flags and linked with the regular object of
-# the other into cnn-gp_amd/lib/ab/lib_<name>.so (tools/gpu.sh ab / tools/variants.sh time it).
+# the other into cnn-gp_amd/lib/ab/lib_<name>.so (tools/gpu.sh ab / tools/ab_variant.sh time it).
 #   bash tools/build_variant.sh NAME "-DFOO=1 -DBAR=0"
 set -eu
 cd "$(dirname "$0")/../cnn-gp_amd/csrc"
