@@ -619,8 +619,12 @@ def cpu_baseline(cfg_name, dtype, seconds):
     return res
 
 
-def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend, probe):
-    """The step loop for one config: Kxx tiles of this rank into a device matrix."""
+def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend, probe,
+                ctl=None):
+    """The step loop for one config: Kxx tiles of this rank into a device matrix.  The
+    barriers around the timed steps and the max over ranks run on ``ctl`` (the gloo side
+    group, host memory): the build has no data-path collective, so the measurement does
+    not depend on RCCL."""
     cfg = importlib.import_module(f"configs.{cfg_name}")
     model = cfg.initial_model.to(dev, dtype)
     C = getattr(cfg, "in_channels", 1)
@@ -634,7 +638,7 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     evaluated = sum(tile_eval_pairs(t, B, n_total) for t in all_tiles)
     mine = sum(tile_eval_pairs(t, B, n_total) for t in tiles)
     ref_sched = sum(min(B, n_total - i * B) * min(B, n_total - j * B) for _, i, j in all_tiles)
-    K = torch.full((n_total, n_total), float("nan"), dtype=torch.float64, device=dev)
+    K = torch.full((n_total, n_total), float("nan"), dtype=dtype, device=dev)
 
     mk = model_kern(model)
 
@@ -645,7 +649,7 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=ctl)
     from cnn_gp import netplan
     netplan.TIMING = [] if rank == 0 and probe else None
     t0 = time.perf_counter()
@@ -654,11 +658,10 @@ def time_config(cfg_name, n1, B, steps, warmup, world, rank, dev, dtype, backend
     torch.cuda.synchronize()
     mine_s = time.perf_counter() - t0
     if world > 1:
-        dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                      device=dev if backend == "nccl" else "cpu")
+        dist.barrier(group=ctl)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=ctl)
     elapsed = float(el.item())
     timing, netplan.TIMING = netplan.TIMING, None
     return dict(model=model, X=X, K=K, n_total=n_total, tiles=tiles, all_tiles=all_tiles,
@@ -683,7 +686,8 @@ def kxx_leg(cfg_name, args, B, world, rank, dev, dtype, backend, probe, group, s
             with_cpu):
     """configs[2] / configs[4]'s network on the headline's harness (Kxx 4096², B = 1024),
     with its own roofline object and CPU baseline"""
-    r2 = time_config(cfg_name, args.n, B, steps, 1, world, rank, dev, dtype, backend, probe)
+    r2 = time_config(cfg_name, args.n, B, steps, 1, world, rank, dev, dtype, backend, probe,
+                     group)
     del r2["K"]
     ranks = gather_rank_stats(r2["rank_stats"], world, group)
     if rank != 0:
@@ -951,7 +955,10 @@ def main(argv=None):
         os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
         tmo = datetime.timedelta(seconds=DIST_TIMEOUT_S)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
+            # host tensors on gloo, device tensors on RCCL (its communicator is created at
+            # the first device collective, i.e. in the full-scale legs): the Kxx legs'
+            # control plane never waits on RCCL, so a broken RCCL costs those legs only
+            dist.init_process_group("cpu:gloo,cuda:nccl", timeout=tmo)
         else:
             dist.init_process_group(backend, timeout=tmo)
         # the status exchange waits for a rank still inside a timed-out collective; the
@@ -999,7 +1006,7 @@ def main(argv=None):
     # --- the headline: BASELINE configs[1] ---
     r = legs.run("headline", lambda: time_config(args.config, args.n, B, args.steps,
                                                  args.warmup, world, rank, dev, dtype,
-                                                 backend, probe))
+                                                 backend, probe, status))
     failed = "error" in r
     if failed:
         full["error"] = r["error"]
@@ -1088,7 +1095,7 @@ def main(argv=None):
             for name in ((args.config,) if args.no_second or args.config == "mnist_as_tf"
                          else (args.config, "mnist_as_tf")):
                 r3 = time_config(name, args.n, B, max(2, args.steps // 2), 1, world, rank, dev,
-                                 torch.float32, backend, False)
+                                 torch.float32, backend, False, status)
                 del r3["K"]
                 f32[name] = {"value": round(r3["value"], 1), "unit": "pairs/s",
                              "ms_per_step": round(r3["ms_step"], 3),
