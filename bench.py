@@ -234,7 +234,17 @@ class Watchdog(threading.Thread):
             return
         print(f"bench.py: watchdog: {self.deadline.hard_s:.0f} s reached, printing the line",
               file=sys.stderr, flush=True)
-        if self.emitter.emit(lambda: self.make_line(watchdog=True)):
+
+        def line():
+            # the main thread may be updating the result while it is read: retry once,
+            # then fall back to the headline keys alone
+            for _ in range(2):
+                try:
+                    return json.loads(json.dumps(self.make_line(watchdog=True)))
+                except Exception:              # noqa: BLE001
+                    time.sleep(0.5)
+            return {"metric": None, "value": None, "watchdog": "line unavailable"}
+        if self.emitter.emit(line):
             self.exit_fn()
 
 
