@@ -32,6 +32,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cnn-gp_amd"), ROOT]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -47,6 +48,34 @@ def mnist_like(n, C, side, seed):
     x[..., :, :4] = 0.0
     x[..., :, -4:] = 0.0
     return x
+
+
+# the leading LEAD x LEAD block of Kxx is kept before the in-place factorisation; a failed
+# solve reports it against a fresh build of the same images (tools/fullscale.py's only
+# source of a "not positive definite" that is not the matrix's own conditioning)
+LEAD = int(os.environ.get("CGP_FS_LEAD", "256"))
+
+
+def lead_report(model, X, lead):
+    """What a failed factorisation saw in the leading block: its own Cholesky on the host
+    (numpy), and the entries that differ from model(X[:L]) built again now."""
+    L = lead.shape[0]
+    got = lead.double().cpu().numpy()
+    upper = np.triu(got) + np.triu(got, 1).T
+    try:
+        np.linalg.cholesky(upper)
+        host = "host Cholesky of the saved block ok"
+    except np.linalg.LinAlgError:
+        host = "host Cholesky of the saved block fails"
+    with torch.no_grad():
+        ref = model(X[:L]).double().cpu().numpy()
+    iu = np.triu_indices(L)
+    rel = np.abs(got[iu] - ref[iu]) / np.abs(ref[iu])
+    bad = np.flatnonzero(~(rel <= 1e-12))
+    first = [(int(iu[0][k]), int(iu[1][k]), float(got[iu][k]), float(ref[iu][k]))
+             for k in bad[:4]]
+    return (f"{host}; leading {L}x{L} upper block vs a fresh build: {len(bad)} entries "
+            f"differ (max rel {np.nanmax(rel) if len(rel) else 0:.3e}), first {first}")
 
 
 def log(rank, msg):
@@ -103,11 +132,18 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
         r = rows.to(K.device)
         saved["Krows"] = torch.where(torch.arange(n, device=K.device)[None, :] >= r[:, None],
                                      K[r], K[:, r].T).to(torch.float64)
+        if LEAD > 0:                 # for the diagnosis of a failed factorisation
+            saved["lead"] = K[:LEAD, :LEAD].clone()
         torch.cuda.synchronize(K.device)
         saved["rows_s"] = time.perf_counter() - t
 
     def solve(K, Yd):
-        A = cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+        try:
+            A = cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+        except np.linalg.LinAlgError as e:
+            if "lead" not in saved:
+                raise
+            raise np.linalg.LinAlgError(f"{e}; {lead_report(model, X, saved['lead'])}") from e
         saved["phases"] = cnn_gp.solve_phases(K.device)
         return A
 
