@@ -939,3 +939,31 @@ def test_var_chain_pointer_handles_match_views(same):
     for v in q1:
         assert q1[v].data_ptr() - base1 == q2[v].data_ptr() - base2
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("cfg", ["mnist_as_tf", "mnist_paper_convnet_gp"])
+def test_forwards_reuse_the_structure_key(cfg):
+    """The plan cache's key (NNGPKernel._structure_key) is reused across forwards while no
+    NNGPKernel changes (kernels._GENERATION): a forward itself writes no module attribute,
+    so the drop-in per-tile loop never re-walks the module tree; a hyper-parameter write
+    changes the key."""
+    from cnn_gp import kernels as K
+    m = configs_util.model(cfg).to(DEV, torch.float64)
+    C, side = specs.GEOMETRY[cfg]
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand((9, C, side, side), generator=g, dtype=torch.float64).to(DEV)
+    y = torch.rand((7, C, side, side), generator=g, dtype=torch.float64).to(DEV)
+    with torch.no_grad():
+        m(x, y, False, False)
+        key = m._structure_key()
+        gen = K._GENERATION[0]
+        for _ in range(2):
+            m(x, y, False, False)
+            m(x, x, True, False)
+            m(x)
+    torch.cuda.synchronize()
+    assert K._GENERATION[0] == gen, "a forward bumped the structure generation"
+    assert m.__dict__["_cgp_skey"] == (gen, key)
+    conv = next(mod for mod in m.modules() if isinstance(mod, cnn_gp.Conv2d))
+    conv.var_bias = float(conv.var_bias) + 0.5
+    assert K._GENERATION[0] != gen and m._structure_key() != key

@@ -32,7 +32,9 @@ mkdir -p "$O"
 step() {   # name limit cmd...
     local name=$1 t=$2; shift 2
     local t0=$SECONDS
-    timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+    # a bench.py run writes its full result beside its log (one file per step: a later
+    # bench step must not overwrite an earlier one's)
+    CGP_BENCH_FULL_OUT="$PWD/$O/${name}_full.json" timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
     local rc=$?
     echo "== $name rc=$rc ($((SECONDS - t0)) s)"
     if [ $rc -ne 0 ]; then tail -n 40 "$O/$name.log"; exit $rc; fi
