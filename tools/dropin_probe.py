@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--config", default="mnist_paper_convnet_gp")
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--tile", type=int, default=200)
+    ap.add_argument("--pin", action="store_true", help="the dataset tensor in pinned memory")
+    ap.add_argument("--dtype", default="f32", choices=["f64", "f32"])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = importlib.import_module(f"configs.{args.config}")
@@ -49,6 +51,10 @@ def main():
     C = getattr(cfg, "in_channels", 1)
     side = 32 if C == 3 else 28
     X = torch.rand((args.n, C, side, side), generator=torch.Generator().manual_seed(0))
+    if args.dtype == "f64":
+        X, model = X.double(), model.double()
+    if args.pin:
+        X = X.pin_memory()
     ds = TensorDataset(X, torch.zeros(args.n, dtype=torch.int64))
 
     def kern(x, x2, same, diag):
