@@ -179,6 +179,11 @@ class NNGPKernel(nn.Module):
         if x.dtype not in (torch.float32, torch.float64):
             raise TypeError(f"cnn_gp kernels compute in float32 or float64, got {x.dtype}")
         out_device = x.device
+        if len(x) == 0 or len(y) == 0:
+            # the reference's torch ops return the empty [N1, N2] / [N1] result for an empty
+            # batch (conv2d on a zero-size batch); there is nothing to evaluate
+            return torch.empty((len(x),) if diag else (len(x), len(y)), dtype=x.dtype,
+                               device=out_device)
         if x.device.type == "cuda":
             dev = x.device
         else:

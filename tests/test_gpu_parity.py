@@ -501,6 +501,10 @@ def test_edge_shapes_and_zero_images():
     # off the diagonal the f32_tiny term keeps zero-variance pairs strictly positive
     assert got[1, 1] == ref[1, 1] == 0.0
     assert np.isfinite(got).all() and (got[1, [0, 2]] > 0).all()
+    # empty batches: the empty result on the inputs' device (the reference's shapes)
+    e = dev(X[:0])
+    assert m(e, dev(X), False, False).shape == (0, 3) and m(e).shape == (0, 0)
+    assert m(e, e, True, True).shape == (0,) and m(dev(X), e, False, False).device.type == "cuda"
 
 
 @pytest.mark.parametrize("cfg", ["mnist_as_tf", "mnist_paper_convnet_gp"])

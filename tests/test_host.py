@@ -499,3 +499,18 @@ def test_diag_iterator_batches_equal_dataloader():
             assert same == (X2 is None) and i == j
             assert torch.equal(xy[0], rx[0]) and torch.equal(xy2[0], ry[0])
             assert torch.equal(xy[1], rx[1])
+
+
+def test_empty_batches_return_empty_results():
+    """An empty image batch on either side gives the empty [N1, N2] (or [N1] diag) result,
+    as the reference's torch ops do (kernels.py:18-57 run on a zero-size batch; checked
+    against the reference in the build container: shapes (0, 3), (3, 0), (0, 0), (0,),
+    float64) — nothing is evaluated, so no device is needed."""
+    import importlib
+    m = importlib.import_module("configs.mnist_as_tf").initial_model.double()
+    e = torch.zeros((0, 1, 28, 28), dtype=torch.float64)
+    x = torch.rand((3, 1, 28, 28), dtype=torch.float64)
+    for args, shape in [((e, x, False, False), (0, 3)), ((x, e, False, False), (3, 0)),
+                        ((e,), (0, 0)), ((e, e, True, True), (0,))]:
+        r = m(*args)
+        assert tuple(r.shape) == shape and r.dtype == torch.float64 and r.device == e.device
