@@ -68,18 +68,20 @@ def tensor_rows(dataset, lo: int, hi: int):
     DatasetFromConfig builds and what save_K is handed); None for any other dataset
     (the caller then collates item by item).  Collating a 200-image batch item by item
     costs ~1-3 ms of host time per tile, several times the kernel's own time at the
-    reference's batch_size 200 (bench.py ``dropin``)."""
-    if isinstance(dataset, TensorDataset):
+    reference's batch_size 200 (bench.py ``dropin``).  The exact classes only: a subclass
+    may override ``__getitem__`` (e.g. a transform), which slicing would bypass."""
+    kind = type(dataset)
+    if kind is TensorDataset:
         return [t[lo:hi] for t in dataset.tensors]
-    if isinstance(dataset, Subset):
+    if kind is Subset:
         idx = dataset.indices[lo:hi]
         if isinstance(idx, range) and idx.step == 1:
             return tensor_rows(dataset.dataset, idx.start, idx.stop)
-        if isinstance(dataset.dataset, TensorDataset):
+        if type(dataset.dataset) is TensorDataset:
             ix = torch.as_tensor(list(idx), dtype=torch.int64)
             return [t[ix] for t in dataset.dataset.tensors]
         return None
-    if isinstance(dataset, ConcatDataset):
+    if kind is ConcatDataset:
         parts, start = [], 0
         for d, end in zip(dataset.datasets, dataset.cumulative_sizes):
             a, b = max(lo, start), min(hi, end)
@@ -156,9 +158,10 @@ class DiagIterator:
         """The DataLoader's batches of X — sliced from the backing tensors when X is a
         TensorDataset / Subset / ConcatDataset of them (tensor_rows), else the DataLoader"""
         n = len(X)
-        if tensor_rows(X, 0, min(n, 1)) is None:
+        out = [tensor_rows(X, lo, min(lo + batch_size, n)) for lo in range(0, n, batch_size)]
+        if any(b is None for b in out):      # e.g. a ConcatDataset with one other part
             return DataLoader(X, batch_size=batch_size)
-        return [tensor_rows(X, lo, min(lo + batch_size, n)) for lo in range(0, n, batch_size)]
+        return out
 
     def __iter__(self):
         return self

@@ -289,7 +289,7 @@ def gather_gram(local: torch.Tensor, N: int, N2: Optional[int], batch_size: int,
         grown[:local.numel()].copy_(local)
         local = grown
     send = local[:cap]
-    staged = local.device.type == "cuda" and dist.get_backend(group) == "gloo"
+    staged = _p2p_staged(group, local.device)
     if staged:
         send = send.cpu()
     gathered = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
@@ -436,9 +436,16 @@ def gram_strip(kern: Callable, X, X2=None, batch_size: int = 4096,
     return out, tiles, sum(tile_cost(t) for t in tiles)
 
 
+def group_moves_device(group) -> bool:
+    """True when the group has RCCL for device tensors: backend "nccl", or a mixed group
+    such as "cpu:gloo,cuda:nccl" (dist.get_backend returns the whole string then)."""
+    return "nccl" in str(dist.get_backend(group))
+
+
 def _p2p_staged(group, tensor_device) -> bool:
-    """gloo moves CPU tensors only: device buffers travel through host memory"""
-    return tensor_device.type == "cuda" and dist.get_backend(group) == "gloo"
+    """gloo moves CPU tensors only: without RCCL in the group, device buffers travel
+    through host memory"""
+    return tensor_device.type == "cuda" and not group_moves_device(group)
 
 
 def gather_strips(strip: Optional[torch.Tensor], plan: List[Tuple[int, int]], n2: int,

@@ -85,6 +85,13 @@ class NNGPKernel(nn.Module):
         fusion = getattr(self, "_cgp_fusion", True)
         exact = getattr(self, "_cgp_exact_relu", False)
         key = (h, w, fusion, exact, self._structure_key())
+        wver = self._weights_version()
+        if self.__dict__.get("_cgp_wver") != wver:
+            # a Conv2d weight buffer changed in place (load_state_dict, mul_, .data = …):
+            # the reference reads self.kernel on every call (kernels.py:92-97), so every
+            # plan built from the old weights goes
+            cache.clear()
+            self.__dict__["_cgp_wver"] = wver
         plan = cache.get(key)
         if plan is None:
             plan = Plan(self, h, w, enable_fusion=fusion, exact_relu=exact)
@@ -105,6 +112,7 @@ class NNGPKernel(nn.Module):
         gen = _GENERATION[0]
         mixture = False
         key = []
+        bufs = []
         stack = [self]
         while stack:
             m = stack.pop()
@@ -114,6 +122,7 @@ class NNGPKernel(nn.Module):
                 key.append(("c", d["kernel_size"], d["stride"], d["padding"], d["dilation"],
                             float(d["var_weight"]), float(d["var_bias"]),
                             d["_buffers"]["kernel"].dtype))
+                bufs.append(d["_buffers"]["kernel"])
             elif isinstance(m, Mixture):
                 mixture = True
                 key.append(("m", tuple(m.proportions())))
@@ -121,9 +130,21 @@ class NNGPKernel(nn.Module):
                 key.append((type(m).__name__, len(d.get("mods", ()))))
             stack.extend(reversed(d["_modules"].values()))
         key = tuple(key)
+        self.__dict__["_cgp_bufs"] = (gen, bufs)
         if not mixture:
             self.__dict__["_cgp_skey"] = (gen, key)     # not through __setattr__
         return key
+
+    def _weights_version(self):
+        """(version counter, address) of every Conv2d weight buffer in the tree, read on
+        the host (no sync): in-place edits bump a tensor's version without touching
+        __setattr__, so the structure key alone cannot see them."""
+        memo = self.__dict__.get("_cgp_bufs")
+        if memo is None or memo[0] != _GENERATION[0]:
+            self.__dict__.pop("_cgp_skey", None)
+            self._structure_key()
+            memo = self.__dict__["_cgp_bufs"]
+        return tuple((b._version, b.data_ptr()) for b in memo[1])
 
     def set_fusion(self, enabled: bool):
         """Enable/disable op fusion in the pair pipeline (for A/B tests; default on)."""
@@ -276,7 +297,7 @@ class NNGPKernel(nn.Module):
             return None
         var, qvar = fused
         return _ImageVariances(x, {v: xx for v, (xx, _) in var.items()}, dict(qvar),
-                               (h, w, x.dtype, plan.flags))
+                               (h, w, x.dtype, plan.flags, self._weights_version()))
 
     def tile_from_variances(self, vx: "_ImageVariances", i0: int, i1: int,
                             vy: "_ImageVariances", j0: int, j1: int, same: bool,
@@ -294,11 +315,14 @@ class NNGPKernel(nn.Module):
         if not (0 <= i0 < i1 <= len(vx) and 0 <= j0 < j1 <= len(vy)):
             raise ValueError(f"tile rows [{i0}, {i1}) x cols [{j0}, {j1}) outside the image "
                              f"sets ({len(vx)}, {len(vy)})")
-        h, w, dtype, flags = vx.key
+        h, w, dtype, flags, wver = vx.key
         plan = self._plan(h, w)
         if plan.flags != flags:
             raise ValueError("tile_from_variances: the model's ReLU mode changed since "
                              "image_variances")
+        if self._weights_version() != wver:
+            raise ValueError("tile_from_variances: a Conv2d weight buffer changed since "
+                             "image_variances (bind the image sets again)")
         net = self._net_plan(plan, torch.empty((), dtype=dtype).element_size())
         x, y = vx.images[i0:i1], vy.images[j0:j1]
         var = {v: (m[i0:i1], vy.var[v][j0:j1]) for v, m in vx.var.items()}

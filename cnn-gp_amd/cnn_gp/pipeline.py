@@ -23,13 +23,17 @@ exact code with the oracle on gloo ranks.
 """
 from __future__ import annotations
 
+import socket
 import time
 from typing import Callable, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
-from .gram import gather_strips, gram_strip, row_slice, strip_cost, strip_plan
+from .gram import (gather_strips, gram_strip, group_moves_device, row_slice, strip_cost,
+                   strip_plan)
+from .solve import ALPHA_CHECK_ROWS, check_alpha, check_rows_index, diag_add, symmetric_rows
 
 __all__ = ("classify_distributed", "kxz_weights", "widening_matrix", "widen_in_place")
 
@@ -92,7 +96,7 @@ def kxz_weights(world: int, n: int, m: int, kernel_pairs_per_s: float,
 
 
 def _bcast(t: torch.Tensor, src: int, group):
-    if t.device.type == "cuda" and dist.get_backend(group) == "gloo":
+    if t.device.type == "cuda" and not group_moves_device(group):
         h = t.cpu()
         dist.broadcast(h, src, group=group)
         t.copy_(h)
@@ -101,12 +105,42 @@ def _bcast(t: torch.Tensor, src: int, group):
     return t
 
 
+def _ctl_device(dev, group):
+    """where the group's small control tensors live: the host when a gloo backend serves
+    host tensors ("gloo", or a mixed "cpu:gloo,cuda:nccl" group), the device under a pure
+    RCCL group (RCCL moves device tensors only)"""
+    return torch.device("cpu") if "gloo" in str(dist.get_backend(group)) else dev
+
+
 def _max_over_ranks(v: float, dev, group) -> float:
-    """max of a host scalar over the group (RCCL reduces device tensors only)"""
-    on = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    t = torch.tensor([v], dtype=torch.float64, device=on)
+    """max of a host scalar over the group"""
+    t = torch.tensor([v], dtype=torch.float64, device=_ctl_device(dev, group))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t)
+
+
+def device_key(dev) -> str:
+    """The physical device a rank computes on: host name plus the GPU's PCI location and
+    UUID (the same for two processes that see one GPU under different visible-device
+    lists), or the host name for a CPU device."""
+    dev = torch.device(dev)
+    host = socket.gethostname()
+    if dev.type != "cuda":
+        return f"{host}:cpu"
+    p = torch.cuda.get_device_properties(dev)
+    return f"{host}:{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}:{p.uuid}"
+
+
+def co_resident_ranks(dev, group, dst: int) -> list:
+    """The ranks of ``group`` other than ``dst`` whose device is dst's device (all_gather
+    of device_key): none in the one-process-per-GPU layout; every rank in a rehearsal
+    whose ranks share one GPU."""
+    keys = [None] * dist.get_world_size(group)
+    dist.all_gather_object(keys, device_key(dev), group=group)
+    return [r for r, k in enumerate(keys) if r != dst and k == keys[dst]]
+
+
+_SOLVE_OK, _SOLVE_FAILED, _SOLVE_WRONG_ALPHA = 0, 1, 2
 
 
 def _sync(dev):
@@ -122,7 +156,10 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          widen: Optional[Callable] = None, log: Optional[Callable] = None,
                          warm: Optional[Callable] = None, cast: Optional[Callable] = None,
                          rank_times: Optional[dict] = None,
-                         pre_solve: Optional[Callable] = None):
+                         pre_solve: Optional[Callable] = None, jitter: float = 0.0,
+                         check_rows: int = ALPHA_CHECK_ROWS,
+                         check_tol: Optional[float] = None,
+                         guard_shared_device: bool = True):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
 
@@ -144,6 +181,21 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     ``pre_solve(K)`` (optional) runs on ``dst`` with the assembled matrix just before the
     solve, outside ``solve_s`` (its time is ``pre_solve_s``): a caller's look at K before a
     solve that factors it in place (e.g. tools/fullscale.py's residual rows).
+
+    ``jitter`` is added to the diagonal of the (widened) Kxx before the solve, as
+    classify_gp.py:66-67 does (load_kern, then diag_add); ``solve`` must solve the system
+    it is handed, exactly.  Its α is then verified on ``check_rows`` fixed rows of that
+    system (solve.check_alpha: backward error ≤ ``check_tol``, default 64·√n·eps): a
+    failure — or any exception in the widening, the pre_solve hook or the solve — is sent
+    to every rank before α, and every rank raises (LinAlgError for a not positive-definite
+    Kxx or a failed check, RuntimeError otherwise on the ranks that did not solve).  α never
+    leaves ``dst`` unchecked.
+
+    ``guard_shared_device``: ranks whose device is dst's device (co_resident_ranks: only in
+    a rehearsal whose ranks share a GPU) wait until dst's solve has returned before they
+    start their Kxz strips, and the Kxz rows are then split evenly.  Factorisations running
+    beside other processes' work on one GPU have returned wrong factors with info = 0
+    (round 5, profiles/r5/r5z_*); with one process per GPU nobody waits.
 
     Each rank binds only the images its strips read: a Kxx strip [r0, r1) touches rows
     and columns >= r0 (X[r0:]), a Kxz strip [z0, z1) the images Z[z0:z1] against all of
@@ -212,40 +264,74 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     res["gather_kxx_s"] = round(time.perf_counter() - t1, 3)
 
     # 3. solve on dst, Kxz strips everywhere (dst's share sized to end with the others)
+    share = co_resident_ranks(dev, group, dst) if (multi and guard_shared_device) else []
+    res["co_resident_ranks"] = share
     rate = strip_cost(n, None, (0, n)) / world / max(el, 1e-9)
-    w = kxz_share if kxz_share is not None else kxz_weights(world, n, m, rate, solve_tflops,
-                                                            dst)
+    if kxz_share is not None:
+        w = kxz_share
+    elif share:                     # dst's solve runs alone: no overlap to size for
+        w = None
+    else:
+        w = kxz_weights(world, n, m, rate, solve_tflops, dst)
     plan_z = strip_plan(m, n, world, weights=w)
     res["plan_kxz"] = plan_z
     z0, z1 = plan_z[rank]
     alpha = None
     failure = None
+    status = _SOLVE_OK
     if rank == dst:
-        if pre_solve is not None:
-            tp = time.perf_counter()
-            pre_solve(K)
-            _sync(dev)
-            res["pre_solve_s"] = round(time.perf_counter() - tp, 4)
-        t2 = time.perf_counter()
-        if K.dtype == out_dtype:
-            Kd = K
-        elif Kwide is not None:
-            Kd = widen_in_place(Kwide, K, cast)
-        else:
-            Kd = conv(K)
-        del K, Kwide
-        _sync(dev)
-        res["widen_s"] = round(time.perf_counter() - t2, 3)
+        t2 = None
+        Kd = None
         try:
-            alpha = solve(Kd, Y.to(dev, out_dtype))
+            if pre_solve is not None:
+                tp = time.perf_counter()
+                pre_solve(K)
+                _sync(dev)
+                res["pre_solve_s"] = round(time.perf_counter() - tp, 4)
+            t2 = time.perf_counter()
+            if K.dtype == out_dtype:
+                Kd = K
+            elif Kwide is not None:
+                Kd = widen_in_place(Kwide, K, cast)
+            else:
+                Kd = conv(K)
+            del K, Kwide
+            if jitter:
+                diag_add(Kd, jitter)
+            _sync(dev)
+            res["widen_s"] = round(time.perf_counter() - t2, 3)
+            idx = check_rows_index(n, check_rows)
+            Krows = symmetric_rows(Kd, idx) if idx else None   # before solve factors Kd
+            Yd = Y.to(dev, out_dtype)
+            alpha = solve(Kd, Yd)
+            if idx:
+                try:
+                    res["alpha_backward_error"] = check_alpha(Krows, idx, alpha, Yd,
+                                                              check_tol)
+                except np.linalg.LinAlgError:
+                    status = _SOLVE_WRONG_ALPHA
+                    raise
         except Exception as e:      # e.g. LinAlgError (not PD): the other ranks must not
             failure = e             # wait for an α that never comes (see step 4)
+            alpha = None
+            if status == _SOLVE_OK:
+                status = _SOLVE_FAILED
         _sync(dev)
-        res["solve_s"] = round(time.perf_counter() - t2, 3)
-        say(f"  solve {res['solve_s']:.2f} s")
+        res["solve_s"] = round(time.perf_counter() - t2, 3) if t2 is not None else None
+        if res["solve_s"] is not None:
+            say(f"  solve {res['solve_s']:.2f} s")
         res["K"] = Kd
         if failure is not None and not multi:
             raise failure
+    if share and (rank == dst or rank in share):
+        # co-resident ranks start their Kxz strips only after dst's solve has returned
+        flag = torch.tensor([status], dtype=torch.int64, device=_ctl_device(dev, group))
+        gr = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+        if rank == dst:
+            for r in share:
+                dist.send(flag, gr(r), group=group)
+        else:
+            dist.recv(flag, gr(dst), group=group)
     if dev.type == "cuda":
         res["peak_bytes_gather_solve"] = int(torch.cuda.max_memory_allocated(dev))
         torch.cuda.reset_peak_memory_stats(dev)      # next: the Kxz strips
@@ -264,13 +350,18 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
     done = time.perf_counter() - t0
 
     # 4. α to every rank, local scores, scores to dst.  The solve's outcome travels first, so
-    # a failed solve raises on every rank instead of leaving them in the broadcast
+    # a failed solve (or an α that fails its check) raises on every rank instead of leaving
+    # them in the broadcast
     ncls = Y.shape[1] if Y.dim() > 1 else 1
     if multi:
-        ok = torch.tensor([0 if failure is None else 1], dtype=torch.int64,
-                          device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        ok = torch.tensor([status], dtype=torch.int64, device=_ctl_device(dev, group))
         dist.broadcast(ok, dst, group=group)
-        if int(ok) != 0 and failure is None:
+        code = int(ok)
+        if code != _SOLVE_OK and failure is None:
+            if code == _SOLVE_WRONG_ALPHA:
+                raise np.linalg.LinAlgError(
+                    f"classify_distributed: the solution on rank {dst} failed its residual "
+                    f"check (a wrong factorisation); no α was broadcast")
             raise RuntimeError(f"classify_distributed: the solve failed on rank {dst}")
     if failure is not None:
         raise failure

@@ -83,7 +83,19 @@ def conv_geometry(mod) -> ConvGeom:
     k, d, s = int(mod.kernel_size), int(mod.dilation), int(mod.stride)
     pad = int(mod.padding)
     offset = -pad + (d if mod.kernel_has_row_of_zeros else 0)
-    w = float(mod.kernel.reshape(-1)[-1].item())
+    kern = mod.kernel.detach().to("cpu", torch.float64).reshape(mod.kernel.shape[-2:])
+    w = float(kern[-1, -1])
+    want = torch.full_like(kern, w)
+    if mod.kernel_has_row_of_zeros:
+        want[0, :] = 0.
+        want[:, 0] = 0.
+    if tuple(mod.kernel.shape[:2]) != (1, 1) or not torch.equal(kern, want):
+        # the HIP kernels run the reference's constant box kernel (kernels.py:75-87); a
+        # buffer edited to anything else has no device path
+        raise NotImplementedError(
+            "Conv2d.kernel must be the constant var_weight/k² box (kernels.py:75-87), with "
+            "the zero first row and column of an even 'same' kernel; got a buffer of shape "
+            f"{tuple(mod.kernel.shape)} that is not")
     return ConvGeom(taps=k, offset=offset, stride=s, dilation=d, weight=w,
                     extent=k + 1 if mod.kernel_has_row_of_zeros else k,
                     bias=float(mod.var_bias))

@@ -8,7 +8,8 @@ triangle the reference's HDF5 files fill — then dpotrs_64.  All through libcnn
 from __future__ import annotations
 
 import ctypes
-from typing import Optional
+import math
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -17,7 +18,8 @@ from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
            "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores",
-           "cast_into", "solve_phases")
+           "cast_into", "solve_phases", "symmetric_rows", "check_rows_index",
+           "alpha_backward_error", "alpha_check_tol", "check_alpha", "last_alpha_check")
 
 
 def _device():
@@ -30,7 +32,90 @@ def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
 
-def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
+# --- the solution check ----------------------------------------------------------------
+# A factorisation can return info = 0 and a wrong factor (round 5: rocSOLVER / rocBLAS
+# factorisations in several processes sharing one GPU, profiles/r5/r5z_*).  scipy never
+# does that (classify_gp.py:24-26), so every solve verifies its α on a few rows of the
+# system it solved: η = ‖K_rows·α − Y_rows‖ / (‖K_rows‖·‖α‖ + ‖Y_rows‖) (Frobenius norms),
+# the normwise backward error of α restricted to those rows.  A backward-stable Cholesky
+# solve gives η of order machine epsilon whatever K's conditioning (≈1e-17 on the
+# 2 048-8 192 SPD matrices of tools/solve_stress.py's kind; the worst-case bound is
+# O(n·eps)); a wrong factor moves every row of K·α, since each row involves all of α.
+
+ALPHA_CHECK_ROWS = 8
+
+
+def alpha_check_tol(n: int) -> float:
+    """The bound on η: 64·√n·eps (3.5e-12 at n = 60 000, 5.5e-14 at n = 37)."""
+    return 64.0 * math.sqrt(max(int(n), 1)) * 2.0 ** -52
+
+
+def check_rows_index(n: int, k: int = ALPHA_CHECK_ROWS) -> list:
+    """k distinct rows of an n-row system, fixed for n (seeded by n): the rows the
+    solution check reads."""
+    k = min(int(k), int(n))
+    if k <= 0:
+        return []
+    g = torch.Generator().manual_seed(int(n))
+    return sorted(torch.randperm(int(n), generator=g)[:k].tolist())
+
+
+def symmetric_rows(K, idx: Sequence[int], jitter: float = 0.0):
+    """Rows ``idx`` of the symmetric matrix whose UPPER triangle K holds (the strictly-lower
+    part — NaN in the reference's Kxx files, data.py:22-29 — is never read), plus
+    ``jitter`` on the diagonal, as a float64 [len(idx), n] tensor on K's device.  Read
+    before a solve that factors K in place."""
+    n = K.shape[0]
+    r = torch.as_tensor(list(idx), dtype=torch.int64, device=K.device)
+    cols = torch.arange(n, device=K.device)[None, :]
+    rows = torch.where(cols >= r[:, None], K[r], K[:, r].T).to(torch.float64)
+    if jitter and len(idx):
+        rows[torch.arange(len(idx), device=K.device), r] += float(jitter)
+    return rows
+
+
+def alpha_backward_error(Krows, idx: Sequence[int], alpha, Y) -> float:
+    """η of ``alpha`` on the saved rows (symmetric_rows) of the system K·α = Y.  On a HIP
+    device the product runs through cgp_gemm_f64; on the host (the CPU tests' gloo
+    ranks) through torch."""
+    n = Krows.shape[1]
+    A = alpha.reshape(n, -1).to(Krows.device, torch.float64)
+    r = torch.as_tensor(list(idx), dtype=torch.int64)
+    Yr = Y.reshape(n, -1)[r.to(Y.device)].to(Krows.device, torch.float64)
+    KA = scores(Krows, A) if Krows.device.type == "cuda" else Krows @ A
+    res = float((KA - Yr).norm())
+    den = float(Krows.norm()) * float(A.norm()) + float(Yr.norm())
+    return res / den if den > 0 else (0.0 if res == 0 else math.inf)
+
+
+def check_alpha(Krows, idx: Sequence[int], alpha, Y, tol: Optional[float] = None) -> float:
+    """Raise ``np.linalg.LinAlgError`` when α's backward error on the saved rows exceeds
+    ``tol`` (default alpha_check_tol(n)) or is not finite; return η otherwise."""
+    if len(idx) == 0:
+        return 0.0
+    n = Krows.shape[1]
+    tol = alpha_check_tol(n) if tol is None else float(tol)
+    eta = alpha_backward_error(Krows, idx, alpha, Y)
+    if not eta <= tol:
+        raise np.linalg.LinAlgError(
+            f"the solution fails the residual check: backward error {eta:.3e} on "
+            f"{len(idx)} rows of K·α = Y exceeds {tol:.3e} (n = {n}); the factorisation "
+            f"returned info = 0 with a wrong factor")
+    return eta
+
+
+# the η of the last checked solve_system per device
+_CHECKS = {}
+
+
+def last_alpha_check(device=None) -> Optional[float]:
+    """η of the last solve_system on ``device`` that ran the solution check (None if none)."""
+    dev = torch.device(device) if device is not None else _device()
+    return _CHECKS.get(_dev_key(dev))
+
+
+def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False,
+                 check_rows: int = ALPHA_CHECK_ROWS, check_tol: Optional[float] = None):
     """Kxx⁻¹ Y for symmetric positive-definite Kxx given by its upper triangle.
 
     Kxx, Y: float64 tensors (classify_gp.py:19-23 asserts the same), on the host or the
@@ -41,7 +126,12 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
     upper triangle becomes the Cholesky factor U (Kxx = UᵀU) that ``predictive_variance``
     reads.  If Kxx is not positive definite, an in-place Kxx is left partly factored.
     Returns the solution on Y's device.  Raises ``np.linalg.LinAlgError`` if Kxx
-    (+ jitter·I) is not positive definite, like scipy.
+    (+ jitter·I) is not positive definite, like scipy — and also if the solution fails
+    the residual check on ``check_rows`` fixed rows (check_alpha: backward error above
+    ``check_tol``, default alpha_check_tol(n); 0 rows turns the check off), which scipy has
+    no need of: a factorisation that returns info = 0 with a wrong factor must not hand
+    back its α (round 5, processes sharing one GPU).  NaN entries in the upper triangle
+    therefore raise too, where scipy (check_finite=False) returns a NaN α.
     """
     assert Kxx.dtype == torch.float64 and Y.dtype == torch.float64, """
     It is important that `Kxx` and `Y` are `float64`s for the inversion,
@@ -59,6 +149,8 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
         else:
             K = Kxx.to(dev).contiguous()
         yd = Y2.to(dev).contiguous()
+        idx = check_rows_index(n, check_rows)
+        Krows = symmetric_rows(K, idx, jitter) if idx else None   # before K is factored
         nrhs = yd.shape[1]
         bt = torch.empty((nrhs, n), dtype=torch.float64, device=dev)
         s = _stream(dev)
@@ -66,6 +158,7 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
         info = N._i64(0)
         ms = (N._f64 * 3)(-1.0, -1.0, -1.0)
         _PHASES.pop(_dev_key(dev), None)        # a failing solve leaves no phases behind
+        _CHECKS.pop(_dev_key(dev), None)
         N.check(N.load().cgp_chol_solve_f64_timed(N.ptr(K), n, n, N.ptr(bt), nrhs, n,
                                                   float(jitter), ctypes.byref(info), ms, s),
                 "cgp_chol_solve_f64")
@@ -75,6 +168,8 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False):
                 f"Kxx is not positive definite (leading minor of order {info.value})")
         sol = torch.empty((n, nrhs), dtype=torch.float64, device=dev)
         N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
+        if idx:
+            _CHECKS[_dev_key(dev)] = check_alpha(Krows, idx, sol, yd, check_tol)
     sol = sol.reshape(n) if vec else sol
     return sol.to(Y.device)
 
@@ -117,7 +212,7 @@ def warm_up_solver(device=None, background: bool = True):
                 n = 6 * 2048 + 64
                 K = torch.zeros((n, n), dtype=torch.float64, device=dev)
                 solve_system(K, torch.ones((n, 10), dtype=torch.float64, device=dev),
-                             jitter=1.0, overwrite_a=True)
+                             jitter=1.0, overwrite_a=True, check_rows=0)
             st.synchronize()
 
     if not background:

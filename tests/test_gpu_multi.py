@@ -212,11 +212,11 @@ def _pipeline_rank(rank, world, port, q, backend="gloo"):
         Y = cnn_gp.one_hot_pm1(torch.randint(0, 10, (200,), generator=g), 10)
 
         def solve(K, Yd):
-            return cnn_gp.solve_system(K, Yd, jitter=1e-6, overwrite_a=True)
+            return cnn_gp.solve_system(K, Yd, overwrite_a=True)
 
         with torch.no_grad():
             res = classify_distributed(gram.model_kern(m), X, Z, Y, solve, cnn_gp.scores,
-                                       batch_size=48, gather_kxz=True)
+                                       batch_size=48, gather_kxz=True, jitter=1e-6)
         out = None
         if (rank or 0) == 0:
             # numpy: pickled by value (a torch tensor on an mp queue travels as a shared

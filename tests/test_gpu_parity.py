@@ -971,3 +971,39 @@ def test_forwards_reuse_the_structure_key(cfg):
     conv = next(mod for mod in m.modules() if isinstance(mod, cnn_gp.Conv2d))
     conv.var_bias = float(conv.var_bias) + 0.5
     assert K._GENERATION[0] != gen and m._structure_key() != key
+
+
+@pytest.mark.parametrize("how", ["mul_", "load_state_dict", "data"])
+def test_in_place_weight_edit_reaches_the_next_forward(how):
+    """The reference reads Conv2d.kernel on every call (kernels.py:92-97): a weight buffer
+    edited in place after a forward (mul_, load_state_dict, .data =) — none of which goes
+    through __setattr__ — changes the next result to the oracle's for the new weight; a
+    bound image set prepared before the edit is refused."""
+    m = configs_util.model("mnist_paper_convnet_gp").to(DEV, torch.float64)
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand((5, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    y = torch.rand((4, 1, 28, 28), generator=g, dtype=torch.float64).to(DEV)
+    with torch.no_grad():
+        k0 = m(x, y, False, False).cpu().numpy()
+        vx = m.image_variances(x)
+        name, conv = next((n, mod) for n, mod in m.named_modules()
+                          if isinstance(mod, cnn_gp.Conv2d))
+        if how == "mul_":
+            conv.kernel.mul_(2)
+        elif how == "load_state_dict":
+            sd = m.state_dict()
+            sd[f"{name}.kernel"] = sd[f"{name}.kernel"] * 2
+            m.load_state_dict(sd)
+        else:
+            conv.kernel.data = conv.kernel.data * 2
+        k1 = m(x, y, False, False).cpu().numpy()
+        kxx = m(x).cpu().numpy()
+    spec = specs.mnist_paper_convnet_gp()
+    spec[1][0][1]["var_weight"] *= 2            # the first conv: twice the weight
+    ref = O.kernel(spec, x.cpu().numpy(), y.cpu().numpy(), False, False)
+    refxx = O.kernel(spec, x.cpu().numpy())
+    assert rel_err(k1, ref) < 1e-8 and rel_err(kxx, refxx) < 1e-8
+    assert rel_err(k0, ref) > 1e-3                # the edit did change the kernel
+    if vx is not None:
+        with pytest.raises(ValueError, match="weight buffer changed"):
+            m.tile_from_variances(vx, 0, 5, vx, 0, 5, True)

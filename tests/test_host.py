@@ -514,3 +514,60 @@ def test_empty_batches_return_empty_results():
                         ((e,), (0, 0)), ((e, e, True, True), (0,))]:
         r = m(*args)
         assert tuple(r.shape) == shape and r.dtype == torch.float64 and r.device == e.device
+
+
+def test_conv_geometry_refuses_a_non_constant_kernel():
+    """the device kernels run the reference's constant box kernel (kernels.py:75-87): an
+    edited buffer of any other shape or value raises instead of being read at one tap"""
+    import torch
+    import cnn_gp
+    from cnn_gp.program import conv_geometry
+    for k in (3, 4):
+        c = cnn_gp.Conv2d(k, var_weight=2.0)
+        geo = conv_geometry(c)
+        assert geo.weight == float(torch.tensor(2.0 / k ** 2, dtype=torch.float32))
+        c.kernel.mul_(2)                          # still a constant box: accepted
+        assert conv_geometry(c).weight == 2 * geo.weight
+        bad = cnn_gp.Conv2d(k)
+        bad.kernel[0, 0, -1, -1] += 1.0
+        with pytest.raises(NotImplementedError):
+            conv_geometry(bad)
+    even = cnn_gp.Conv2d(4)
+    even.kernel[0, 0, 0, 0] = 1.0                 # the zero row of an even 'same' kernel
+    with pytest.raises(NotImplementedError):
+        conv_geometry(even)
+
+
+def test_tensor_rows_exact_classes_and_mixed_concat():
+    """a TensorDataset subclass with its own __getitem__ goes through the DataLoader (its
+    transform applies); a ConcatDataset mixing a TensorDataset with another dataset type
+    yields the DataLoader's batches, never None"""
+    from torch.utils.data import ConcatDataset, DataLoader, Dataset, TensorDataset
+    from cnn_gp.data import DiagIterator, tensor_rows
+
+    class Doubled(TensorDataset):
+        def __getitem__(self, i):
+            x, y = super().__getitem__(i)
+            return 2 * x, y
+
+    class Plain(Dataset):
+        def __init__(self, x, y):
+            self.x, self.y = x, y
+
+        def __len__(self):
+            return len(self.x)
+
+        def __getitem__(self, i):
+            return self.x[i], self.y[i]
+
+    x = torch.arange(24, dtype=torch.float64).reshape(6, 1, 2, 2)
+    y = torch.arange(6)
+    assert tensor_rows(Doubled(x, y), 0, 3) is None
+    d = Doubled(x, y)
+    got = [b for _, (_, b), _ in DiagIterator(4, d)]
+    want = list(DataLoader(d, batch_size=4))
+    assert all(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) for a, b in zip(got, want))
+    mixed = ConcatDataset([TensorDataset(x[:3], y[:3]), Plain(x[3:], y[3:])])
+    got = [b for _, (_, b), _ in DiagIterator(2, mixed)]
+    assert len(got) == 3 and all(b is not None for b in got)
+    assert torch.equal(torch.cat([b[0] for b in got]), x)

@@ -17,6 +17,7 @@ from oracle import nngp_oracle as O
 from oracle import specs
 
 N, M, B = 37, 13, 8
+JITTER = 1e-6
 
 
 def _free_port():
@@ -41,8 +42,8 @@ def _fns():
     def kern(x, x2, same):
         return torch.from_numpy(O.kernel(spec, x.numpy(), x2.numpy(), same, False))
 
-    def solve(K, Y):
-        return torch.from_numpy(O.solve_upper(K.numpy(), Y.numpy(), 1e-6))
+    def solve(K, Y):                    # the jitter is the pipeline's (classify_gp.py:66-67)
+        return torch.from_numpy(O.solve_upper(K.numpy(), Y.numpy(), 0.0))
 
     def scores(Kz, A):
         return Kz @ A
@@ -63,7 +64,7 @@ def _run(world, rank, port, q, gather, dst=0, dtype=torch.float64):
         X, Z, Y = _data()
         kern, solve, scores = _fns()
         res = classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B, device="cpu",
-                                   gather_kxz=gather, dst=dst, dtype=dtype)
+                                   gather_kxz=gather, dst=dst, dtype=dtype, jitter=JITTER)
         if rank == dst:
             # numpy: pickled by value (a torch tensor on an mp queue travels as a shared
             # memory handle, which dies with this process)
@@ -110,7 +111,8 @@ def test_gloo_pipeline_matches_single_process(world, gather, dst):
     # against the oracle end to end: Kxx, the posv solve, argmax(Kxz @ A)
     spec = specs.mnist_paper_convnet_gp()
     Kref = O.kernel(spec, _data()[0].numpy())
-    np.testing.assert_allclose(res["K"][iu], Kref[iu], rtol=1e-12)
+    # res["K"] is the system the solve saw: Kxx + jitter·I (classify_gp.py:66-67)
+    np.testing.assert_allclose(res["K"][iu], (Kref + JITTER * np.eye(N))[iu], rtol=1e-12)
     X, Z, Y = _data()
     A = O.solve_upper(Kref, Y.numpy(), 1e-6)
     Sref = O.kernel(spec, Z.numpy(), X.numpy(), False, False) @ A
@@ -139,7 +141,9 @@ def test_gloo_pipeline_float32_kernels_widened_in_place():
     assert np.array_equal(res["K"][iu], single["K"][iu])
     assert np.array_equal(res["alpha"], single["alpha"])
     Kref = O.kernel(specs.mnist_paper_convnet_gp(), _data()[0].numpy())
-    assert np.array_equal(res["K"][iu], Kref.astype(np.float32).astype(np.float64)[iu])
+    K32 = Kref.astype(np.float32).astype(np.float64)
+    K32.flat[::N + 1] += JITTER
+    assert np.array_equal(res["K"][iu], K32[iu])
     assert res["Kxz"].dtype == np.float32
 
 
@@ -265,3 +269,142 @@ def test_gloo_pipeline_failed_solve_raises_on_every_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == {0: "LinAlgError", 1: "RuntimeError", 2: "RuntimeError"}
+
+
+def _run_guarded(world, rank, port, q, mode, backend="gloo"):
+    """one rank of the solve-guard tests: ``mode`` "order" (the solve sleeps, the ranks
+    report when their Kxz strips started), "wrong_alpha" (the solve returns a perturbed α),
+    "pre_solve_raises" (the hook before the solve raises)"""
+    import sys
+    import time
+    from conftest import PKG, ROOT
+    sys.path[:0] = [PKG, ROOT]
+    from cnn_gp.pipeline import classify_distributed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        X, Z, Y = _data()
+        kern0, solve0, scores = _fns()
+        first_kxz = []
+
+        def kern(x, x2, same):        # a Kxz tile: its rows are images of Z
+            if not first_kxz and len(x) and any(torch.equal(x[0], z) for z in Z):
+                first_kxz.append(time.time())
+            return kern0(x, x2, same)
+
+        solve_end = []
+
+        def solve(K, Yd):
+            a = solve0(K, Yd)
+            if mode == "order":
+                time.sleep(1.5)
+            if mode == "wrong_alpha":      # a wrong factor's α: 1e-6 relative noise
+                g = torch.Generator().manual_seed(0)
+                a = a * (1 + 1e-6 * torch.randn(a.shape, generator=g, dtype=a.dtype))
+            solve_end.append(time.time())
+            return a
+
+        def pre_solve(K):
+            if mode == "pre_solve_raises":
+                raise ValueError("the hook fails")
+
+        try:
+            res = classify_distributed(kern, X, Z, Y, solve, scores, batch_size=B,
+                                       device="cpu", jitter=JITTER, pre_solve=pre_solve)
+            out = ("ok", dist.get_backend(), first_kxz[:1], solve_end,
+                   None if res is None else res["co_resident_ranks"],
+                   None if res is None else res.get("alpha_backward_error"))
+        except np.linalg.LinAlgError as e:
+            out = ("LinAlgError", str(e)[:80])
+        except RuntimeError as e:
+            out = ("RuntimeError" if "solve failed" in str(e) else repr(e),)
+        except ValueError as e:
+            out = ("ValueError", str(e))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(world, mode, backend="gloo"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_guarded, args=(world, r, port, q, mode, backend))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_gloo_pipeline_co_resident_ranks_wait_for_the_solve():
+    """ranks on dst's device (here: three CPU ranks of one host) start their Kxz strips only
+    after dst's solve has returned; α is checked (backward error far below the bound)"""
+    from cnn_gp.solve import alpha_check_tol
+    got = _spawn(3, "order")
+    assert all(v[0] == "ok" for v in got.values()), got
+    end = got[0][3][0]
+    assert got[0][4] == [1, 2]
+    started = [got[r][2][0] for r in (1, 2) if got[r][2]]   # 13 rows on 8-row cuts: one
+    assert started and min(started) >= end, (started, end)  # rank holds no Kxz rows
+    eta = got[0][5]
+    assert eta is not None and 0 <= eta < alpha_check_tol(N) / 100
+
+
+def test_gloo_pipeline_wrong_alpha_raises_on_every_rank():
+    """an α that fails the residual check (a factorisation returning info = 0 and a wrong
+    factor) is never broadcast: LinAlgError on every rank"""
+    got = _spawn(3, "wrong_alpha")
+    assert {r: v[0] for r, v in got.items()} == {0: "LinAlgError", 1: "LinAlgError",
+                                                 2: "LinAlgError"}, got
+    assert "residual check" in got[0][1] and "residual check" in got[1][1]
+
+
+def test_gloo_pipeline_failing_pre_solve_raises_on_every_rank():
+    """an exception in the hook before the solve reaches every rank (no rank is left in
+    the status broadcast)"""
+    got = _spawn(3, "pre_solve_raises")
+    assert got == {0: ("ValueError", "the hook fails"), 1: ("RuntimeError",),
+                   2: ("RuntimeError",)}
+
+
+def test_mixed_backend_group_string():
+    """under a mixed group ("cpu:gloo,cuda:gloo" here; "cpu:gloo,cuda:nccl" in bench.py)
+    dist.get_backend returns the whole string and the pipeline still runs end to end"""
+    got = _spawn(2, "order", backend="cpu:gloo,cuda:gloo")
+    assert all(v[0] == "ok" for v in got.values()), got
+    assert "gloo" in got[0][1] and "," in got[0][1]
+
+
+def test_symmetric_rows_and_check_alpha():
+    """rows of the symmetric matrix from its upper triangle only (NaN below), jitter on the
+    diagonal; the check passes scipy's α and rejects a perturbed one"""
+    import scipy.linalg
+    from cnn_gp.solve import (alpha_backward_error, check_alpha, check_rows_index,
+                              symmetric_rows)
+    rng = np.random.default_rng(1)
+    n = 50
+    G = rng.random((n, 8))
+    A = G @ G.T / 8 + 0.05 * np.eye(n)
+    K = A.copy()
+    K[np.tril_indices(n, -1)] = np.nan
+    idx = check_rows_index(n, 8)
+    assert len(set(idx)) == 8 and idx == check_rows_index(n, 8) and max(idx) < n
+    rows = symmetric_rows(torch.from_numpy(K), idx, 0.25)
+    want = A[idx] + 0.25 * np.eye(n)[idx]
+    assert np.array_equal(rows.numpy(), want)
+    Y = rng.standard_normal((n, 3))
+    a = scipy.linalg.solve(A + 0.25 * np.eye(n), Y, assume_a="pos")
+    eta = check_alpha(rows, idx, torch.from_numpy(a), torch.from_numpy(Y))
+    assert eta < 1e-15
+    bad = torch.from_numpy(a * (1 + 1e-7 * rng.standard_normal(a.shape)))
+    assert alpha_backward_error(rows, idx, bad, torch.from_numpy(Y)) > 1e-10
+    with pytest.raises(np.linalg.LinAlgError):
+        check_alpha(rows, idx, bad, torch.from_numpy(Y))
+    with pytest.raises(np.linalg.LinAlgError):
+        check_alpha(rows, idx, torch.full_like(bad, float("nan")), torch.from_numpy(Y))
+    assert check_rows_index(3, 8) == [0, 1, 2] and check_rows_index(5, 0) == []

@@ -139,7 +139,7 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
 
     def solve(K, Yd):
         try:
-            A = cnn_gp.solve_system(K, Yd, jitter=jitter, overwrite_a=True)
+            A = cnn_gp.solve_system(K, Yd, overwrite_a=True)   # jitter: the pipeline's
         except np.linalg.LinAlgError as e:
             if "lead" not in saved:
                 raise
@@ -158,7 +158,7 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                    log=lambda msg: log(rank, msg),
                                    warm=lambda: cnn_gp.warm_up_solver(dev),
                                    cast=cnn_gp.cast_into, rank_times=times,
-                                   pre_solve=residual_rows)
+                                   pre_solve=residual_rows, jitter=jitter)
     wall = time.perf_counter() - t0
     ranks = [times]
     if world > 1:
@@ -171,6 +171,8 @@ def fullscale(config="mnist_as_tf", n=60000, m=10000, tile=4096, jitter=0.0, spo
                                     "total_s")})
     ph = saved.get("phases")
     res.update(solve_s=out["solve_s"], kxz_s_rank0=out["kxz_s_rank"],
+               alpha_backward_error=out.get("alpha_backward_error"),
+               co_resident_ranks=out.get("co_resident_ranks"),
                solve_tflops=round(n ** 3 / 3 / out["solve_s"] / 1e12, 2),
                harness_s=round(saved["rows_s"], 4))
     if ph is not None:              # the solve's own HIP-event phases (solve.solve_phases)
