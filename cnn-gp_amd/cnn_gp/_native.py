@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNNGP_LIB",
                           os.path.join(os.path.dirname(_HERE), "lib", "libcnngp.so"))
 
-CGP_ABI_VERSION = 10
+CGP_ABI_VERSION = 11
 CGP_FLAG_EXACT_RELU = 1
 CGP_FLAG_GENERIC_CONV = 2
 CGP_FLAG_NET_DUAL = 4
@@ -141,6 +141,8 @@ SIGNATURES = {
     "cgp_chol_solve_f64_timed": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _f64,
                                         ctypes.POINTER(_i64), ctypes.POINTER(_f64), _vp]),
     "cgp_gemm_f64": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
+    "cgp_sym_mirror_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "cgp_sym_residual_f64": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
     "cgp_argmax_rows_f64": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "cgp_pred_var_f64": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp]),
     "cgp_net_geometry": (_i32, [_i32] * 7),

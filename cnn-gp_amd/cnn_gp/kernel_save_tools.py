@@ -9,6 +9,10 @@ or the in-memory stand-in used by the tests).
 """
 from __future__ import annotations
 
+import collections
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 from .data import DiagIterator, ProductIterator, print_timings
@@ -27,9 +31,20 @@ def create_h5py_dataset(f, batch_size, name, diag, N, N2):
 
 
 def save_K(f, kern, name, X, X2, diag, batch_size, worker_rank=0, n_workers=1,
-           print_interval=2.):
+           print_interval=2., overlap=2):
     """Evaluate this worker's tiles with ``kern(x, x2, same, diag) -> np.ndarray`` and
-    write them into dataset ``name`` (created if absent; skipped if it exists)."""
+    write them into dataset ``name`` (created if absent; skipped if it exists).
+
+    ``overlap`` (default 2): up to that many tiles are in flight at once, each kern call
+    on a helper thread with a HIP stream of its own (torch's current stream is per
+    thread), so one tile's host work — the caller's pageable H2D copies, forward's launch
+    calls, the synchronous copy back, the finiteness check and the dataset write — runs
+    while the GPU evaluates another (save_kernel.py:21-24's kern synchronises per tile,
+    which left the GPU idle for 30-43% of a B = 200 build, bench.py ``dropin``).  Tiles
+    are still checked and written in the reference's order, every tile's values are the
+    same bits (a tile depends on its own images only), and an exception of a kern call
+    or of the finiteness check surfaces in that order.  ``overlap=1`` calls kern on the
+    calling thread, one tile at a time, as kernel_save_tools.py:49-58 does."""
     if name in f.keys():
         print("Skipping {} (group exists)".format(name))
         return
@@ -42,14 +57,56 @@ def save_K(f, kern, name, X, X2, diag, batch_size, worker_rank=0, n_workers=1,
         it = ProductIterator(batch_size, X, X2, worker_rank=worker_rank, n_workers=n_workers)
     it = print_timings(it, desc=f"{name} (worker {worker_rank}/{n_workers})",
                        print_interval=print_interval)
-    for same, (i, (x, _y)), (j, (x2, _y2)) in it:
-        k = kern(x, x2, same, diag)
+
+    def write(i, j, x, x2, k):
         if not np.all(np.isfinite(k)):
             raise FloatingPointError(f"About to write a nan or inf for {i},{j} in {name}")
         if diag:
             out[0, i:i + len(x)] = k
         else:
             out[0, i:i + len(x), j:j + len(x2)] = k
+
+    if overlap <= 1:
+        for same, (i, (x, _y)), (j, (x2, _y2)) in it:
+            write(i, j, x, x2, kern(x, x2, same, diag))
+        return
+    call = _on_own_stream(kern)
+    pending = collections.deque()
+    with ThreadPoolExecutor(max_workers=int(overlap),
+                            thread_name_prefix="cgp-save-K") as pool:
+        try:
+            for same, (i, (x, _y)), (j, (x2, _y2)) in it:
+                pending.append((i, j, x, x2, pool.submit(call, x, x2, same, diag)))
+                if len(pending) >= overlap:
+                    i_, j_, a_, b_, fut = pending.popleft()
+                    write(i_, j_, a_, b_, fut.result())
+            while pending:
+                i_, j_, a_, b_, fut = pending.popleft()
+                write(i_, j_, a_, b_, fut.result())
+        finally:
+            for *_, fut in pending:        # an error above: nothing more is written
+                fut.cancel()
+
+
+def _on_own_stream(kern):
+    """kern wrapped to run under a HIP stream of the calling thread's own (created on the
+    thread's first call) when a GPU is visible; plain kern otherwise."""
+    import torch
+    if not torch.cuda.is_available():
+        return kern
+    dev = torch.cuda.current_device()          # the caller's device, not device 0
+    local = threading.local()
+
+    def call(x, x2, same, diag):
+        s = getattr(local, "stream", None)
+        if s is None:
+            torch.cuda.set_device(dev)
+            s = local.stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            k = kern(x, x2, same, diag)
+        return k
+
+    return call
 
 
 def merge_nan_fill(dest, sources):

@@ -226,6 +226,11 @@ class NNGPKernel(nn.Module):
         lib = N.load()
         net = None if diag else self._net_plan(plan, x.element_size())
         if net is not None and VAR_CHAIN:
+            # the same launches from a recipe built once per tile shape and stream (record
+            # upload, state buffers and argument structs done once; netplan.TileRecipe)
+            rec = net.tile_recipe(plan, x, y, n1, n2, same, plan.flags, stream)
+            if rec is not None:
+                return rec.run(x, y, stream)
             # every variance map in one launch (cgp_var_chain_*), scaled (1/16) x-side copies
             # included (kernels.py:44-49 moments, then the program on each image)
             fused = plan.run_variances_fused(x, y, n1, n2, same, stream, net.need_var,

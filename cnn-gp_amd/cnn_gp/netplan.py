@@ -25,9 +25,11 @@ writes it, and convs consume their whole input into the scratch before writing.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import dataclasses
 import os
+import threading
 from typing import Optional
 
 import torch
@@ -53,6 +55,11 @@ FUSE_REDUCE = os.environ.get("CGP_NET_FUSE_REDUCE", "1") != "0"
 MAX_LDS_BYTES = 160 * 1024
 # state buffers below this size are allocated without asking for the free memory
 SMALL_STATE_BYTES = 512 << 20
+# Tile recipes (TileRecipe): a forward's launch sequence kept per (tile shape, stream)
+# while its persistent buffers (variance maps, stage states) take at most RECIPE_MAX_BYTES,
+# at most RECIPE_SLOTS per NetPlan (least recently used dropped first).  0 turns them off.
+RECIPE_MAX_BYTES = int(os.environ.get("CGP_RECIPE_MAX_MB", "512")) << 20
+RECIPE_SLOTS = 8
 
 
 class Unsupported(Exception):
@@ -817,6 +824,8 @@ class NetPlan:
             else:
                 run_all(stream)
 
+        launch.args = launches           # TileRecipe rewrites x / y / out per call
+        launch.states = states
         return launch, out
 
     def quarter_vars(self, dtype, flags: int = 0) -> set:
@@ -834,10 +843,103 @@ class NetPlan:
             self.__dict__["_quarter_used"] = used
         return set(used)
 
+    def tile_recipe(self, plan, x, y, n1: int, n2: int, same: bool, flags: int, stream):
+        """The cached TileRecipe of a forward of this shape on ``stream`` (built on first
+        use), or None when its persistent buffers would exceed RECIPE_MAX_BYTES or the
+        variance chain cannot run the program (forward then takes the per-call path)."""
+        if RECIPE_MAX_BYTES <= 0:
+            return None
+        key = (n1, n2, bool(same), tuple(x.shape[1:]), x.dtype, x.device, flags, stream)
+        lock = self.__dict__.setdefault("_recipe_lock", threading.Lock())
+        with lock:
+            cache = self.__dict__.setdefault("_recipes", collections.OrderedDict())
+            if key in cache:
+                cache.move_to_end(key)
+                return cache[key]
+            rec = TileRecipe.build(self, plan, x, y, n1, n2, same, flags, stream)
+            if rec is None:
+                return None
+            cache[key] = rec
+            while len(cache) > RECIPE_SLOTS:
+                cache.popitem(last=False)
+            return rec
+
     def run(self, x, y, var, n1: int, n2: int, same: bool, stream, flags: int = 0,
             out: Optional[torch.Tensor] = None, qvar: Optional[dict] = None):
         """K tile [n1, n2] of the pairs (x_i, y_j).  var: value -> (xx [n1,..], yy [n2,..])
         for every value in ``need_var``."""
         launch, out = self.prepare(x, y, var, n1, n2, same, flags, out, qvar)
         launch(stream)
+        return out
+
+
+class TileRecipe:
+    """One forward's whole launch sequence for a tile shape on one stream, built once and
+    replayed: the variance chain (cgp_var_chain_*) into a persistent map buffer, then the
+    net stages (cgp_net_*) whose op records point into that buffer — so the records are
+    uploaded once, the stage-state buffers are allocated once, and a call only writes the
+    images' and the output's addresses into the prebuilt argument structs and issues the
+    launches.  save_kernel.py's loop (kernel_save_tools.py:49-58, a forward per tile and a
+    synchronous copy back) spent 0.11 ms (ConvNet) to 0.29 ms (mnist_as_tf) of host time
+    per B = 200 tile building these (tools/dropin_probe.py), GPU idle meanwhile.
+
+    Replays on one stream are ordered by that stream: the next call's variance chain
+    overwrites the maps only after this call's net kernels have read them.  A lock keeps
+    each call's launch sequence contiguous when threads share a stream."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+
+    @classmethod
+    def build(cls, net, plan, x, y, n1, n2, same, flags, stream):
+        from .program import DevPtr
+        need = set(net.need_var)
+        quarter = net.quarter_vars(x.dtype, flags) & need
+        chain = plan._var_chain(need, quarter, x.device)
+        if chain is None or chain["lds"] * x.element_size() > 64 * 1024 or \
+                x.shape[2] * x.shape[3] > 1024:
+            return None
+        m2 = 0 if same else n2
+        n = n1 + m2
+        item = x.element_size()
+        vbytes = (n * chain["total"] + n1 * chain["qtotal"]) * item
+        units = net.units(n1, n2, same)
+        sbytes = sum(units * st.load_stride for st in net.stages[1:]) * item
+        if vbytes + sbytes > RECIPE_MAX_BYTES:
+            return None
+        r = cls()
+        r.shape = (n1, n2, tuple(x.shape[1:]), x.dtype, x.device)
+        r.same = bool(same)
+        r.vbuf = torch.empty((vbytes // item,), dtype=x.dtype, device=x.device)
+        a = N.VarArgs()
+        a.out, a.ops = r.vbuf.data_ptr(), chain["ops"].data_ptr()
+        a.n1, a.n2, a.store_total = n1, m2, chain["total"]
+        a.nops, a.channels, a.h, a.w = chain["nops"], x.shape[1], x.shape[2], x.shape[3]
+        a.lds_elems, a.scratch = chain["lds"], chain["scratch"]
+        r.va = a
+        r.var_fn = getattr(N.load(), f"cgp_var_chain_{plan._sfx(x.dtype)}")
+        r.chain_ops = chain["ops"]
+        var, qvar = {}, {}
+        shapes = plan.prog.shapes
+        for v, off in chain["store"].items():
+            ho, wo = shapes[v]
+            px = DevPtr(r.vbuf, n * off * item)
+            var[v] = (px, px if same else DevPtr(r.vbuf, (n * off + n1 * ho * wo) * item))
+        for v, off in chain["qstore"].items():
+            qvar[v] = DevPtr(r.vbuf, (n * chain["total"] + n1 * off) * item)
+        out = torch.empty((n1, n2), dtype=x.dtype, device=x.device)
+        r.launch, _ = net.prepare(x, y, var, n1, n2, same, flags, out, qvar or None)
+        r.args = r.launch.args
+        return r
+
+    def run(self, x, y, stream):
+        n1, n2, _, _, _ = self.shape
+        out = torch.empty((n1, n2), dtype=x.dtype, device=x.device)
+        xp, yp, op = x.data_ptr(), y.data_ptr(), out.data_ptr()
+        with self.lock:
+            self.va.x, self.va.y = xp, yp
+            N.check(self.var_fn(self.va, stream), "cgp_var_chain")
+            for a in self.args:
+                a.x, a.y, a.out, a.ldo = xp, yp, op, n2
+            self.launch(stream)
         return out

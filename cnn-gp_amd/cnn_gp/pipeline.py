@@ -33,7 +33,7 @@ import torch.distributed as dist
 
 from .gram import (gather_strips, gram_strip, group_moves_device, row_slice, strip_cost,
                    strip_plan)
-from .solve import ALPHA_CHECK_ROWS, check_alpha, check_rows_index, diag_add, symmetric_rows
+from .solve import check_alpha, diag_add, mirror_upper
 
 __all__ = ("classify_distributed", "kxz_weights", "widening_matrix", "widen_in_place")
 
@@ -157,8 +157,7 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                          warm: Optional[Callable] = None, cast: Optional[Callable] = None,
                          rank_times: Optional[dict] = None,
                          pre_solve: Optional[Callable] = None, jitter: float = 0.0,
-                         check_rows: int = ALPHA_CHECK_ROWS,
-                         check_tol: Optional[float] = None,
+                         check: bool = True, check_tol: Optional[float] = None,
                          guard_shared_device: bool = True):
     """Kxx of X, α = solve(Kxx, Y), scores = Kxz @ α for Z against X, over the process
     group (or one process).
@@ -184,12 +183,15 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
 
     ``jitter`` is added to the diagonal of the (widened) Kxx before the solve, as
     classify_gp.py:66-67 does (load_kern, then diag_add); ``solve`` must solve the system
-    it is handed, exactly.  Its α is then verified on ``check_rows`` fixed rows of that
-    system (solve.check_alpha: backward error ≤ ``check_tol``, default 64·√n·eps): a
-    failure — or any exception in the widening, the pre_solve hook or the solve — is sent
-    to every rank before α, and every rank raises (LinAlgError for a not positive-definite
-    Kxx or a failed check, RuntimeError otherwise on the ranks that did not solve).  α never
-    leaves ``dst`` unchecked.
+    it is handed, exactly.  With ``check`` (default) the system is mirrored into Kxx's
+    strictly-lower triangle first (solve.mirror_upper: the NaN tiles of the reference's
+    layout) and α is verified against all of it (solve.check_alpha: backward error ≤
+    ``check_tol``, default 16·√n·eps) — ``solve`` may factor the upper triangle in place
+    but must leave the strictly-lower one alone (solve_system and scipy's posv do).  A
+    failed check — or any exception in the widening, the pre_solve hook or the solve — is
+    sent to every rank before α, and every rank raises (LinAlgError for a not
+    positive-definite Kxx or a failed check, RuntimeError otherwise on the ranks that did
+    not solve).  α never leaves ``dst`` unchecked.
 
     ``guard_shared_device``: ranks whose device is dst's device (co_resident_ranks: only in
     a rehearsal whose ranks share a GPU) wait until dst's solve has returned before they
@@ -300,14 +302,12 @@ def classify_distributed(kern: Callable, X, Z, Y: torch.Tensor, solve: Callable,
                 diag_add(Kd, jitter)
             _sync(dev)
             res["widen_s"] = round(time.perf_counter() - t2, 3)
-            idx = check_rows_index(n, check_rows)
-            Krows = symmetric_rows(Kd, idx) if idx else None   # before solve factors Kd
+            dK = mirror_upper(Kd) if check else None        # before solve factors Kd
             Yd = Y.to(dev, out_dtype)
             alpha = solve(Kd, Yd)
-            if idx:
+            if check:
                 try:
-                    res["alpha_backward_error"] = check_alpha(Krows, idx, alpha, Yd,
-                                                              check_tol)
+                    res["alpha_backward_error"] = check_alpha(Kd, dK, alpha, Yd, check_tol)
                 except np.linalg.LinAlgError:
                     status = _SOLVE_WRONG_ALPHA
                     raise

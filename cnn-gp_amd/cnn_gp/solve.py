@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import math
-from typing import Optional, Sequence
+from typing import Optional
 
 import numpy as np
 import torch
@@ -18,8 +18,8 @@ from . import _native as N
 
 __all__ = ("solve_system", "diag_add", "load_kern", "print_accuracy", "predict",
            "accuracy", "one_hot_pm1", "predictive_variance", "warm_up_solver", "scores",
-           "cast_into", "solve_phases", "symmetric_rows", "check_rows_index",
-           "alpha_backward_error", "alpha_check_tol", "check_alpha", "last_alpha_check")
+           "cast_into", "solve_phases", "mirror_upper", "alpha_backward_error",
+           "alpha_check_tol", "check_alpha", "last_alpha_check")
 
 
 def _device():
@@ -34,73 +34,83 @@ def _stream(dev):
 
 # --- the solution check ----------------------------------------------------------------
 # A factorisation can return info = 0 and a wrong factor (round 5: rocSOLVER / rocBLAS
-# factorisations in several processes sharing one GPU, profiles/r5/r5z_*).  scipy never
-# does that (classify_gp.py:24-26), so every solve verifies its α on a few rows of the
-# system it solved: η = ‖K_rows·α − Y_rows‖ / (‖K_rows‖·‖α‖ + ‖Y_rows‖) (Frobenius norms),
-# the normwise backward error of α restricted to those rows.  A backward-stable Cholesky
-# solve gives η of order machine epsilon whatever K's conditioning (≈1e-17 on the
-# 2 048-8 192 SPD matrices of tools/solve_stress.py's kind; the worst-case bound is
-# O(n·eps)); a wrong factor moves every row of K·α, since each row involves all of α.
-
-ALPHA_CHECK_ROWS = 8
-
+# factorisations in several processes sharing one GPU, profiles/r5/r5z_*, r6/r6b_*).
+# scipy never does that (classify_gp.py:24-26), so every solve verifies its α against the
+# whole system it solved: the system is mirrored into the strictly-lower triangle before
+# the factorisation (cgp_sym_mirror_f64; the solve reads and overwrites only the upper
+# one), and afterwards r = Y − K·α is formed from that triangle in one pass
+# (cgp_sym_residual_f64).  The measure is the normwise backward error
+#     η = ‖r‖ / (‖K‖_F·‖α‖ + ‖Y‖)      (Frobenius norms),
+# which a backward-stable Cholesky solve keeps at the rounding level whatever K's
+# conditioning (2.4-2.6e-17 on the gloo rehearsal's 16 384² NNGP matrices); a wrong
+# factor leaves rows of the system unsatisfied — possibly only a few, e.g. the rows of one
+# corrupted trailing-update tile, which is why no row sample is used.
 
 def alpha_check_tol(n: int) -> float:
-    """The bound on η: 64·√n·eps (3.5e-12 at n = 60 000, 5.5e-14 at n = 37)."""
-    return 64.0 * math.sqrt(max(int(n), 1)) * 2.0 ** -52
+    """The bound on η: 16·√n·eps (8.6e-13 at n = 60 000, 2.1e-14 at n = 37)."""
+    return 16.0 * math.sqrt(max(int(n), 1)) * 2.0 ** -52
 
 
-def check_rows_index(n: int, k: int = ALPHA_CHECK_ROWS) -> list:
-    """k distinct rows of an n-row system, fixed for n (seeded by n): the rows the
-    solution check reads."""
-    k = min(int(k), int(n))
-    if k <= 0:
-        return []
-    g = torch.Generator().manual_seed(int(n))
-    return sorted(torch.randperm(int(n), generator=g)[:k].tolist())
-
-
-def symmetric_rows(K, idx: Sequence[int], jitter: float = 0.0):
-    """Rows ``idx`` of the symmetric matrix whose UPPER triangle K holds (the strictly-lower
-    part — NaN in the reference's Kxx files, data.py:22-29 — is never read), plus
-    ``jitter`` on the diagonal, as a float64 [len(idx), n] tensor on K's device.  Read
-    before a solve that factors K in place."""
+def mirror_upper(K):
+    """K[i][j] = K[j][i] for every i > j, in place (the strictly-lower triangle — NaN
+    tiles in the reference's files, data.py:22-29 — takes the system the upper triangle
+    holds); returns the diagonal as float64 on K's device.  A float64 contiguous device
+    matrix goes through cgp_sym_mirror_f64, a host matrix through torch."""
     n = K.shape[0]
-    r = torch.as_tensor(list(idx), dtype=torch.int64, device=K.device)
-    cols = torch.arange(n, device=K.device)[None, :]
-    rows = torch.where(cols >= r[:, None], K[r], K[:, r].T).to(torch.float64)
-    if jitter and len(idx):
-        rows[torch.arange(len(idx), device=K.device), r] += float(jitter)
-    return rows
+    if K.device.type == "cuda":
+        if K.dtype != torch.float64 or not K.is_contiguous():
+            raise ValueError("mirror_upper: a contiguous float64 device matrix")
+        d = torch.empty((n,), dtype=torch.float64, device=K.device)
+        with torch.cuda.device(K.device):
+            N.call("cgp_sym_mirror_f64", N.ptr(K), n, K.stride(0), N.ptr(d),
+                   _stream(K.device))
+        return d
+    il = torch.tril_indices(n, n, -1)
+    K[il[0], il[1]] = K[il[1], il[0]]
+    return K.diagonal().to(torch.float64).clone()
 
 
-def alpha_backward_error(Krows, idx: Sequence[int], alpha, Y) -> float:
-    """η of ``alpha`` on the saved rows (symmetric_rows) of the system K·α = Y.  On a HIP
-    device the product runs through cgp_gemm_f64; on the host (the CPU tests' gloo
-    ranks) through torch."""
-    n = Krows.shape[1]
-    A = alpha.reshape(n, -1).to(Krows.device, torch.float64)
-    r = torch.as_tensor(list(idx), dtype=torch.int64)
-    Yr = Y.reshape(n, -1)[r.to(Y.device)].to(Krows.device, torch.float64)
-    KA = scores(Krows, A) if Krows.device.type == "cuda" else Krows @ A
-    res = float((KA - Yr).norm())
-    den = float(Krows.norm()) * float(A.norm()) + float(Yr.norm())
+def _residual_t(K, d, xt, yt):
+    """(r = Yᵀ − (K·X)ᵀ as [nrhs, n], ‖K‖_F) from K's strictly-lower triangle and d, with
+    X and Y given transposed ([nrhs, n] contiguous float64, on K's device)."""
+    n = K.shape[0]
+    if K.device.type == "cuda":
+        r = yt.clone()
+        ss = torch.zeros((1,), dtype=torch.float64, device=K.device)
+        with torch.cuda.device(K.device):
+            N.call("cgp_sym_residual_f64", N.ptr(K), n, K.stride(0), N.ptr(d), N.ptr(xt),
+                   N.ptr(r), xt.shape[0], n, N.ptr(ss), _stream(K.device))
+        fro = math.sqrt(2.0 * float(ss) + float((d * d).sum()))
+        return r, fro
+    L = torch.tril(K.to(torch.float64), -1)
+    kx = L @ xt.T + L.T @ xt.T + d[:, None] * xt.T
+    return yt - kx.T, math.sqrt(2.0 * float((L * L).sum()) + float((d * d).sum()))
+
+
+def alpha_backward_error(K, d, alpha, Y) -> float:
+    """η of ``alpha`` for the system whose strictly-lower triangle (mirror_upper) and
+    diagonal ``d`` K holds: ‖Y − K·α‖ / (‖K‖_F·‖α‖ + ‖Y‖)."""
+    n = K.shape[0]
+    xt = alpha.reshape(n, -1).to(K.device, torch.float64).T.contiguous()
+    yt = Y.reshape(n, -1).to(K.device, torch.float64).T.contiguous()
+    r, fro = _residual_t(K, d.to(K.device, torch.float64), xt, yt)
+    res = float(r.norm())
+    den = fro * float(xt.norm()) + float(yt.norm())
     return res / den if den > 0 else (0.0 if res == 0 else math.inf)
 
 
-def check_alpha(Krows, idx: Sequence[int], alpha, Y, tol: Optional[float] = None) -> float:
-    """Raise ``np.linalg.LinAlgError`` when α's backward error on the saved rows exceeds
-    ``tol`` (default alpha_check_tol(n)) or is not finite; return η otherwise."""
-    if len(idx) == 0:
-        return 0.0
-    n = Krows.shape[1]
+def check_alpha(K, d, alpha, Y, tol: Optional[float] = None) -> float:
+    """Raise ``np.linalg.LinAlgError`` when α's backward error for the system K·α = Y
+    (K's strictly-lower triangle and diagonal d, see mirror_upper) exceeds ``tol``
+    (default alpha_check_tol(n)) or is not finite; return η otherwise."""
+    n = K.shape[0]
     tol = alpha_check_tol(n) if tol is None else float(tol)
-    eta = alpha_backward_error(Krows, idx, alpha, Y)
+    eta = alpha_backward_error(K, d, alpha, Y)
     if not eta <= tol:
         raise np.linalg.LinAlgError(
-            f"the solution fails the residual check: backward error {eta:.3e} on "
-            f"{len(idx)} rows of K·α = Y exceeds {tol:.3e} (n = {n}); the factorisation "
-            f"returned info = 0 with a wrong factor")
+            f"the solution fails the residual check: backward error {eta:.3e} of K·α = Y "
+            f"exceeds {tol:.3e} (n = {n}); the factorisation returned info = 0 with a "
+            f"wrong factor")
     return eta
 
 
@@ -115,7 +125,7 @@ def last_alpha_check(device=None) -> Optional[float]:
 
 
 def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False,
-                 check_rows: int = ALPHA_CHECK_ROWS, check_tol: Optional[float] = None):
+                 check: bool = True, check_tol: Optional[float] = None):
     """Kxx⁻¹ Y for symmetric positive-definite Kxx given by its upper triangle.
 
     Kxx, Y: float64 tensors (classify_gp.py:19-23 asserts the same), on the host or the
@@ -126,12 +136,15 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False,
     upper triangle becomes the Cholesky factor U (Kxx = UᵀU) that ``predictive_variance``
     reads.  If Kxx is not positive definite, an in-place Kxx is left partly factored.
     Returns the solution on Y's device.  Raises ``np.linalg.LinAlgError`` if Kxx
-    (+ jitter·I) is not positive definite, like scipy — and also if the solution fails
-    the residual check on ``check_rows`` fixed rows (check_alpha: backward error above
-    ``check_tol``, default alpha_check_tol(n); 0 rows turns the check off), which scipy has
-    no need of: a factorisation that returns info = 0 with a wrong factor must not hand
-    back its α (round 5, processes sharing one GPU).  NaN entries in the upper triangle
-    therefore raise too, where scipy (check_finite=False) returns a NaN α.
+    (+ jitter·I) is not positive definite, like scipy — and, with ``check`` (default),
+    also if the solution fails the residual check against the whole system (check_alpha:
+    backward error above ``check_tol``, default alpha_check_tol(n)), which scipy has no
+    need of: a factorisation that returns info = 0 with a wrong factor must not hand back
+    its α (round 5, processes sharing one GPU).  NaN entries in the upper triangle
+    therefore raise too, where scipy (check_finite=False) returns a NaN α.  The check
+    mirrors the system into the strictly-lower triangle of the matrix it factors (for an
+    in-place solve: Kxx's, where the reference's files hold NaN) and costs two passes over
+    that triangle (≈ 10 ms at n = 60 000, beside a ≈ 1.3 s factorisation).
     """
     assert Kxx.dtype == torch.float64 and Y.dtype == torch.float64, """
     It is important that `Kxx` and `Y` are `float64`s for the inversion,
@@ -149,12 +162,15 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False,
         else:
             K = Kxx.to(dev).contiguous()
         yd = Y2.to(dev).contiguous()
-        idx = check_rows_index(n, check_rows)
-        Krows = symmetric_rows(K, idx, jitter) if idx else None   # before K is factored
         nrhs = yd.shape[1]
         bt = torch.empty((nrhs, n), dtype=torch.float64, device=dev)
         s = _stream(dev)
         N.call("cgp_transpose_f64", N.ptr(yd), n, nrhs, N.ptr(bt), s)
+        if check:                       # the system, kept below the diagonal (+ jitter)
+            d = mirror_upper(K)
+            if jitter:
+                d += float(jitter)
+            yt = bt.clone()
         info = N._i64(0)
         ms = (N._f64 * 3)(-1.0, -1.0, -1.0)
         _PHASES.pop(_dev_key(dev), None)        # a failing solve leaves no phases behind
@@ -168,8 +184,18 @@ def solve_system(Kxx, Y, jitter: float = 0.0, overwrite_a: bool = False,
                 f"Kxx is not positive definite (leading minor of order {info.value})")
         sol = torch.empty((n, nrhs), dtype=torch.float64, device=dev)
         N.call("cgp_transpose_f64", N.ptr(bt), nrhs, n, N.ptr(sol), s)
-        if idx:
-            _CHECKS[_dev_key(dev)] = check_alpha(Krows, idx, sol, yd, check_tol)
+        if check:
+            r, fro = _residual_t(K, d, bt, yt)
+            res = float(r.norm())
+            den = fro * float(bt.norm()) + float(yt.norm())
+            eta = res / den if den > 0 else (0.0 if res == 0 else math.inf)
+            tol = alpha_check_tol(n) if check_tol is None else float(check_tol)
+            if not eta <= tol:
+                raise np.linalg.LinAlgError(
+                    f"the solution fails the residual check: backward error {eta:.3e} of "
+                    f"K·α = Y exceeds {tol:.3e} (n = {n}); the factorisation returned "
+                    f"info = 0 with a wrong factor")
+            _CHECKS[_dev_key(dev)] = eta
     sol = sol.reshape(n) if vec else sol
     return sol.to(Y.device)
 
@@ -212,7 +238,7 @@ def warm_up_solver(device=None, background: bool = True):
                 n = 6 * 2048 + 64
                 K = torch.zeros((n, n), dtype=torch.float64, device=dev)
                 solve_system(K, torch.ones((n, 10), dtype=torch.float64, device=dev),
-                             jitter=1.0, overwrite_a=True, check_rows=0)
+                             jitter=1.0, overwrite_a=True, check=False)
             st.synchronize()
 
     if not background:

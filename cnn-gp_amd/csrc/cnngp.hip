@@ -772,6 +772,120 @@ __global__ __launch_bounds__(kBlock) void row_sumsq_sub_kernel(const double* __r
     }
 }
 
+// ---- the solution check (cgp_sym_mirror_f64 / cgp_sym_residual_f64) ------------------
+// The solve reads only the row-major upper triangle of K and overwrites it with the
+// factor; the strictly-lower triangle is free (NaN tiles in the reference's files).  The
+// mirror copies the system there before the factorisation, so after the solve the whole
+// residual Y − K·X can be formed in one pass over the lower triangle: every row of the
+// system is checked, not a sample (a wrong factor can be wrong in a few rows only).
+constexpr int kSymT = 64;                 // tile edge
+constexpr int kSymLd = kSymT + 1;         // LDS pitch (doubles)
+constexpr int kSymRhs = 16;               // right-hand sides per residual launch
+constexpr int kSymChunk = 8;              // tiles of one row panel per residual workgroup
+
+// workgroup (I, J), J <= I: the upper block (J, I) read row by row into LDS, written
+// transposed as the lower block (I, J) row by row (both coalesced); a diagonal tile
+// copies its own upper part down and stores the diagonal.  Reads (upper, incl. the
+// diagonal) and writes (strictly lower) never meet across workgroups.
+__global__ __launch_bounds__(kBlock) void sym_mirror_kernel(double* __restrict__ k, long long n,
+                                                           long long ld,
+                                                           double* __restrict__ diag) {
+    const int I = blockIdx.x, J = blockIdx.y;
+    if (J > I) return;
+    __shared__ double t[kSymT * kSymLd];
+    const long long r0 = (long long)J * kSymT, c0 = (long long)I * kSymT;
+    for (int e = threadIdx.x; e < kSymT * kSymT; e += kBlock) {
+        const int r = e >> 6, c = e & 63;
+        const long long gr = r0 + r, gc = c0 + c;
+        t[r * kSymLd + c] = (gr < n && gc < n && gc >= gr) ? k[gr * ld + gc] : 0.0;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kSymT * kSymT; e += kBlock) {
+        const int rr = e >> 6, cc = e & 63;          // destination (c0 + rr, r0 + cc)
+        const long long gr = c0 + rr, gc = r0 + cc;
+        if (gr < n && gc < n) {
+            if (gc < gr)
+                k[gr * ld + gc] = t[cc * kSymLd + rr];
+            else if (gc == gr)
+                diag[gr] = t[cc * kSymLd + rr];
+        }
+    }
+}
+
+// r[q][i] −= Σ_j (L + Lᵀ + diag(d))[i][j]·x[q][j], L = the strictly-lower triangle of K;
+// sumsq[0] += Σ L[i][j]² over the tiles read.  Workgroup (I, c): row panel I, tiles
+// J in [c·kSymChunk, min((c+1)·kSymChunk, I + 1)).  Per tile (staged in LDS): the rows of
+// panel I gain L_IJ·x_J (registers, over the chunk), the columns of J gain L_IJᵀ·x_I (one
+// atomic add per column and right-hand side).  Wave g handles right-hand sides g, g+4, …
+// (uniform per wave: the x reads are LDS broadcasts).
+__global__ __launch_bounds__(kBlock) void sym_residual_kernel(const double* __restrict__ k,
+                                                             long long n, long long ld,
+                                                             const double* __restrict__ diag,
+                                                             const double* __restrict__ x,
+                                                             double* r, int nrhs, long long ldx,
+                                                             double* sumsq) {
+    const int I = blockIdx.x, c = blockIdx.y;
+    const int jt0 = c * kSymChunk;
+    if (jt0 > I) return;
+    const int jt1 = min(jt0 + kSymChunk, I + 1);
+    __shared__ double t[kSymT * kSymLd];
+    __shared__ double xi[kSymRhs * kSymT], xj[kSymRhs * kSymT];
+    __shared__ double red[kBlock / 64];
+    const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    const long long i0 = (long long)I * kSymT;
+    for (int e = tid; e < nrhs * kSymT; e += kBlock) {
+        const int q = e >> 6, l = e & 63;
+        xi[e] = (i0 + l < n) ? x[q * ldx + i0 + l] : 0.0;
+    }
+    double racc[kSymRhs / 4] = {};
+    double ss = 0.0;
+    for (int J = jt0; J < jt1; ++J) {
+        const long long j0 = (long long)J * kSymT;
+        __syncthreads();                               // the previous tile's readers
+        for (int e = tid; e < kSymT * kSymT; e += kBlock) {
+            const int rr = e >> 6, cc = e & 63;
+            const long long gr = i0 + rr, gc = j0 + cc;
+            const double v = (gr < n && gc < gr) ? k[gr * ld + gc] : 0.0;
+            t[rr * kSymLd + cc] = v;
+            ss = __builtin_fma(v, v, ss);
+        }
+        for (int e = tid; e < nrhs * kSymT; e += kBlock) {
+            const int q = e >> 6, l = e & 63;
+            xj[e] = (j0 + l < n) ? x[q * ldx + j0 + l] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < kSymRhs / 4; ++m) {
+            const int q = g + 4 * m;
+            if (q < nrhs) {
+                double a = 0.0, b = 0.0;
+                for (int cc = 0; cc < kSymT; ++cc) {
+                    a = __builtin_fma(t[lane * kSymLd + cc], xj[q * kSymT + cc], a);   // rows
+                    b = __builtin_fma(t[cc * kSymLd + lane], xi[q * kSymT + cc], b);   // columns
+                }
+                racc[m] += a;
+                if (j0 + lane < n) atomicAdd(&r[q * ldx + j0 + lane], -b);
+            }
+        }
+    }
+    if (i0 + lane < n) {
+        const bool has_diag = I >= jt0 && I < jt1;
+#pragma unroll
+        for (int m = 0; m < kSymRhs / 4; ++m) {
+            const int q = g + 4 * m;
+            if (q < nrhs) {
+                double v = racc[m];
+                if (has_diag) v = __builtin_fma(diag[i0 + lane], xi[q * kSymT + lane], v);
+                atomicAdd(&r[q * ldx + i0 + lane], -v);
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    if (lane == 0) red[g] = ss;
+    __syncthreads();
+    if (tid == 0 && sumsq) atomicAdd(sumsq, red[0] + red[1] + red[2] + red[3]);
+}
+
 // ---- the variance chain (cgp_var_chain_*): every per-image variance map of a network in
 // one launch.  A workgroup walks image g through the op list in LDS (slots from the host);
 // the stored maps go to out (layout in cnngp.h).  Same rounding as the layer kernels it
@@ -1524,6 +1638,40 @@ int cgp_transpose_f64(const double* src, int64_t rows, int64_t cols, double* dst
     hipLaunchKernelGGL(transpose_kernel, dim3(grid_for(rows * cols)), dim3(kBlock), 0,
                        as_stream(stream), src, (long long)rows, (long long)cols, dst);
     return check_launch("transpose_kernel");
+}
+
+int cgp_sym_mirror_f64(double* k, int64_t n, int64_t ldk, double* diag, void* stream) {
+    if (!k || !diag || n <= 0 || ldk < n)
+        return fail(CGP_EINVAL, "sym_mirror: bad arguments (n=%lld ldk=%lld)", (long long)n,
+                    (long long)ldk);
+    const long long tiles = (n + kSymT - 1) / kSymT;
+    if (tiles > 65535) return fail(CGP_EINVAL, "sym_mirror: n=%lld too large", (long long)n);
+    hipLaunchKernelGGL(sym_mirror_kernel, dim3((unsigned)tiles, (unsigned)tiles), dim3(kBlock),
+                       0, as_stream(stream), k, (long long)n, (long long)ldk, diag);
+    return check_launch("sym_mirror_kernel");
+}
+
+int cgp_sym_residual_f64(const double* k, int64_t n, int64_t ldk, const double* diag,
+                         const double* x, double* r, int64_t nrhs, int64_t ldx, double* sumsq,
+                         void* stream) {
+    if (!k || !diag || !x || !r || !sumsq || n <= 0 || ldk < n || nrhs <= 0 || ldx < n)
+        return fail(CGP_EINVAL, "sym_residual: bad arguments (n=%lld nrhs=%lld)",
+                    (long long)n, (long long)nrhs);
+    const long long tiles = (n + kSymT - 1) / kSymT;
+    const long long chunks = (tiles + kSymChunk - 1) / kSymChunk;
+    if (tiles > 65535) return fail(CGP_EINVAL, "sym_residual: n=%lld too large", (long long)n);
+    hipStream_t s = as_stream(stream);
+    for (int64_t q0 = 0; q0 < nrhs; q0 += kSymRhs) {
+        // the tiles' squares once: only the first group of right-hand sides adds them up
+        hipLaunchKernelGGL(sym_residual_kernel, dim3((unsigned)tiles, (unsigned)chunks),
+                           dim3(kBlock), 0, s, k, (long long)n, (long long)ldk, diag,
+                           x + q0 * ldx, r + q0 * ldx,
+                           (int)std::min<int64_t>(kSymRhs, nrhs - q0), (long long)ldx,
+                           q0 == 0 ? sumsq : nullptr);
+        const int rc = check_launch("sym_residual_kernel");
+        if (rc) return rc;
+    }
+    return CGP_OK;
 }
 
 int cgp_chol_solve_f64(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,

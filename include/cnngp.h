@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define CGP_ABI_VERSION 10
+#define CGP_ABI_VERSION 11
 
 /* error codes */
 #define CGP_OK 0
@@ -214,6 +214,24 @@ int cgp_chol_last_phases(void* stream, double* ms);
 int cgp_chol_solve_f64_timed(double* k, int64_t n, int64_t ldk, double* bt, int64_t nrhs,
                              int64_t ldb, double jitter, int64_t* info, double* phase_ms,
                              void* stream);
+/*
+ * ABI 11: the solution check (no reference counterpart: scipy's solve never hands back a
+ * wrong factor silently; rocSOLVER / rocBLAS factorisations in processes sharing one GPU
+ * have, with info = 0 — round 5).  classify_gp.py:17-27's system K·X = Y, K given by its
+ * row-major upper triangle, the triangle cgp_chol_solve_f64 reads and overwrites:
+ *   cgp_sym_mirror_f64: K[i][j] = K[j][i] for every i > j (the strictly-lower triangle,
+ *     unread by the solve, takes the system) and diag[i] = K[i][i] ([n], device).  Call
+ *     before the factorisation (after any jitter: diag then holds K + jitter·I's).
+ *   cgp_sym_residual_f64: r −= (L + Lᵀ + diag(d))·X with L the strictly-lower triangle
+ *     of k: X and r are [nrhs][ldx] row-major (transposed, as cgp_chol_solve_f64's bt);
+ *     r holds Y on entry and Y − K·X on return; *sumsq (device) += Σ_{i>j} K[i][j]² (so
+ *     ‖K‖_F² = 2·sumsq + Σ d²).  Atomic accumulation: the last bits vary run to run.
+ * One pass over the lower triangle each (n²/2 · 8 bytes read; the mirror writes as much).
+ */
+int cgp_sym_mirror_f64(double* k, int64_t n, int64_t ldk, double* diag, void* stream);
+int cgp_sym_residual_f64(const double* k, int64_t n, int64_t ldk, const double* diag,
+                         const double* x, double* r, int64_t nrhs, int64_t ldx, double* sumsq,
+                         void* stream);
 /*
  * Row-major C[m][n] = A[m][kdim] @ B[kdim][n] (fp64, rocBLAS) — the Kxz @ α product of
  * print_accuracy, classify_gp.py:39-42.

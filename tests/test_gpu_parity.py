@@ -599,13 +599,21 @@ def test_solve_blocked_cholesky_matches_scipy(n):
     rng = np.random.default_rng(1)
     Y = rng.standard_normal((n, 10))
     Kd = torch.from_numpy(K).to(DEV)
-    sol = cnn_gp.solve_system(Kd, torch.from_numpy(Y).to(DEV), jitter=0.5, overwrite_a=True)
+    sol = cnn_gp.solve_system(Kd, torch.from_numpy(Y).to(DEV), jitter=0.5, overwrite_a=True,
+                              check=False)
     ref = scipy.linalg.solve(A + 0.5 * np.eye(n), Y, assume_a="pos", lower=False)
     np.testing.assert_allclose(sol.cpu().numpy(), ref, rtol=1e-10, atol=1e-12)
     U = np.triu(Kd.cpu().numpy())
     Uref = scipy.linalg.cholesky(A + 0.5 * np.eye(n), lower=False)
     np.testing.assert_allclose(U, Uref, rtol=1e-10, atol=1e-12)
-    assert np.isnan(Kd.cpu().numpy()[np.tril_indices(n, -1)]).all()   # never written
+    low = np.tril_indices(n, -1)
+    assert np.isnan(Kd.cpu().numpy()[low]).all()   # the factorisation never writes there
+    # with the solution check (default): the same factor and solution bits, the system
+    # mirrored into the strictly-lower triangle
+    K2 = torch.from_numpy(K).to(DEV)
+    sol2 = cnn_gp.solve_system(K2, torch.from_numpy(Y).to(DEV), jitter=0.5, overwrite_a=True)
+    assert torch.equal(sol, sol2) and torch.equal(torch.triu(K2), torch.triu(Kd))
+    assert np.array_equal(K2.cpu().numpy()[low], A[low])
 
 
 @pytest.mark.parametrize("bad", [5, 2047, 2048, 4000])
@@ -1007,3 +1015,134 @@ def test_in_place_weight_edit_reaches_the_next_forward(how):
     if vx is not None:
         with pytest.raises(ValueError, match="weight buffer changed"):
             m.tile_from_variances(vx, 0, 5, vx, 0, 5, True)
+
+
+@pytest.mark.parametrize("cfg", ["mnist_paper_convnet_gp", "mnist_as_tf"])
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_tile_recipes_equal_the_per_call_path(cfg, dt, monkeypatch):
+    """forward through a cached TileRecipe (netplan: records uploaded once, persistent
+    variance / state buffers, only the image and output addresses rewritten per call) is
+    bit-equal to the per-call path, over repeated calls of one shape with new images,
+    ragged and diagonal tiles, and two streams; a recipe is built once per shape and
+    stream"""
+    from cnn_gp import netplan
+    m = configs_util.model(cfg).to(DEV, dt)
+    C, side = specs.GEOMETRY[cfg]
+    g = torch.Generator().manual_seed(21)
+    imgs = [torch.rand((n, C, side, side), generator=g).to(DEV, dt) for n in (24, 24, 17, 24)]
+    cases = [(imgs[0], imgs[1], False), (imgs[1], imgs[0], False), (imgs[2], imgs[3], False),
+             (imgs[3], imgs[3], True), (imgs[0], imgs[0], True), (imgs[2], imgs[2], True)]
+
+    def run_all():
+        outs = []
+        with torch.no_grad():
+            for x, y, same in cases:
+                outs.append(m(x, y, same, False).clone())
+            s2 = torch.cuda.Stream()
+            with torch.cuda.stream(s2):
+                outs.append(m(imgs[1], imgs[2], False, False).clone())
+                outs.append(m(imgs[0], imgs[3], False, False).clone())
+            torch.cuda.current_stream().wait_stream(s2)
+        torch.cuda.synchronize()
+        return [o.cpu() for o in outs]
+
+    got = run_all()
+    net = m._net_plan(m._plan(side, side), torch.empty((), dtype=dt).element_size())
+    recs = net.__dict__.get("_recipes", {})
+    assert net is not None and 4 <= len(recs) <= netplan.RECIPE_SLOTS
+    got2 = run_all()                               # replays of the same recipes
+    assert len(net.__dict__["_recipes"]) == len(recs)
+    monkeypatch.setattr(netplan, "RECIPE_MAX_BYTES", 0)
+    want = run_all()
+    for a, b, c in zip(got, got2, want):
+        assert torch.equal(a, c) and torch.equal(b, c)
+
+
+def test_save_K_overlap_bit_equal_on_device():
+    """save_K's helper threads (overlap 2 and 4, a HIP stream each) write the same float32
+    dataset as the serial loop with the device model (save_kernel.py:21-24's kern)"""
+    from cnn_gp import save_K
+    model = configs_util.model("mnist_as_tf").cuda()
+    g = torch.Generator().manual_seed(4)
+    X = torch.rand((70, 1, 28, 28), generator=g)
+    ds = torch.utils.data.TensorDataset(X, torch.zeros(len(X)))
+
+    def kern(x, x2, same, diag):
+        with torch.no_grad():
+            return model(x.cuda(), x2.cuda(), same, diag).detach().cpu().numpy()
+
+    class F:
+        def __init__(self):
+            self.d = {}
+
+        def keys(self):
+            return self.d.keys()
+
+        def create_dataset(self, name, shape, dtype, fillvalue, chunks, maxshape):
+            self.d[name] = np.full(shape, fillvalue, dtype=dtype)
+            return self.d[name]
+
+    outs = []
+    for ov in (1, 2, 4):
+        f = F()
+        save_K(f, kern, "Kxx", ds, None, False, 16, print_interval=1e9, overlap=ov)
+        outs.append(f.d["Kxx"])
+    assert np.isfinite(outs[0][0][np.triu_indices(70)]).all()
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+
+
+@pytest.mark.parametrize("n,nrhs", [(1, 1), (63, 10), (64, 3), (65, 17), (200, 10),
+                                    (4100, 10)])
+def test_sym_mirror_and_residual_kernels(n, nrhs):
+    """cgp_sym_mirror_f64 copies the upper triangle below the diagonal (NaN lower part in,
+    exact copy out) and returns the diagonal; cgp_sym_residual_f64 forms Y − K·X and ‖K‖_F
+    from the lower triangle alone (the upper one replaced by garbage) against numpy"""
+    from cnn_gp.solve import _residual_t, mirror_upper
+    rng = np.random.default_rng(n + nrhs)
+    A = rng.standard_normal((n, n))
+    A = A + A.T
+    K = A.copy()
+    K[np.tril_indices(n, -1)] = np.nan
+    Kd = torch.from_numpy(K).to(DEV)
+    d = mirror_upper(Kd)
+    torch.cuda.synchronize()
+    assert np.array_equal(Kd.cpu().numpy(), A) and np.array_equal(d.cpu().numpy(), np.diag(A))
+    Kd[torch.triu_indices(n, n, 0)[0], torch.triu_indices(n, n, 0)[1]] = float("nan")
+    X = rng.standard_normal((n, nrhs))
+    Y = rng.standard_normal((n, nrhs))
+    r, fro = _residual_t(Kd, d, torch.from_numpy(X.T.copy()).to(DEV),
+                         torch.from_numpy(Y.T.copy()).to(DEV))
+    want = Y - A @ X
+    scale = np.abs(A).sum(1).max() * np.abs(X).max() + 1
+    assert np.abs(r.cpu().numpy().T - want).max() < 1e-13 * scale
+    assert abs(fro - np.linalg.norm(A)) < 1e-12 * np.linalg.norm(A)
+
+
+def test_solve_check_catches_a_few_wrong_rows_on_device():
+    """solve_system's check: a correct solve passes with a rounding-level backward error,
+    the lower triangle then holds the system; an α from a factor wrong in one 4-row block
+    (a corrupted trailing-update tile) fails check_alpha on the device kernels"""
+    import scipy.linalg
+    from cnn_gp.solve import alpha_check_tol, check_alpha, last_alpha_check, mirror_upper
+    n = 4100
+    rng = np.random.default_rng(5)
+    G = rng.random((n, 32))
+    A = G @ G.T / 32 + 0.05 * np.eye(n)
+    K = A.copy()
+    K[np.tril_indices(n, -1)] = np.nan
+    Kd = torch.from_numpy(K).to(DEV)
+    Y = rng.standard_normal((n, 10))
+    a = cnn_gp.solve_system(Kd, torch.from_numpy(Y).to(DEV), overwrite_a=True)
+    eta = last_alpha_check(DEV)
+    assert eta is not None and eta < alpha_check_tol(n) / 100
+    low = np.tril_indices(n, -1)
+    assert np.array_equal(Kd.cpu().numpy()[low], A[low])          # the mirrored system
+    E = np.zeros_like(A)
+    E[3000:3004, 3000:3004] = 1e-9 * rng.standard_normal((4, 4))
+    bad = scipy.linalg.solve(A + E + E.T, Y, assume_a="pos")
+    K2 = torch.from_numpy(K).to(DEV)
+    d = mirror_upper(K2)
+    assert check_alpha(K2, d, a, torch.from_numpy(Y).to(DEV)) < alpha_check_tol(n) / 100
+    with pytest.raises(np.linalg.LinAlgError, match="residual check"):
+        check_alpha(K2, d, torch.from_numpy(bad).to(DEV), torch.from_numpy(Y).to(DEV))

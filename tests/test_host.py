@@ -571,3 +571,50 @@ def test_tensor_rows_exact_classes_and_mixed_concat():
     got = [b for _, (_, b), _ in DiagIterator(2, mixed)]
     assert len(got) == 3 and all(b is not None for b in got)
     assert torch.equal(torch.cat([b[0] for b in got]), x)
+
+
+@pytest.mark.parametrize("overlap", [2, 3, 5])
+def test_save_K_overlap_writes_the_serial_files(overlap):
+    """tiles in flight on helper threads (save_K's default overlap = 2): the same dataset
+    as the serial reference loop, tiles written in the reference's order, and the first
+    failing tile's FloatingPointError raised with nothing written after it"""
+    import threading
+    rng = np.random.default_rng(3)
+    X = torch.from_numpy(rng.random((37, 1, 4, 4)))
+    ds = torch.utils.data.TensorDataset(X, torch.zeros(len(X)))
+    threads = set()
+
+    def kern(x, x2, same, diag):
+        threads.add(threading.get_ident())
+        k = (x.reshape(len(x), -1) @ x2.reshape(len(x2), -1).T).numpy()
+        return np.diag(k).copy() if diag else k
+
+    ref, got = FakeFile(), FakeFile()
+    save_K(ref, kern, "Kxx", ds, None, False, 8, print_interval=1e9, overlap=1)
+    save_K(got, kern, "Kxx", ds, None, False, 8, print_interval=1e9, overlap=overlap)
+    np.testing.assert_array_equal(got.d["Kxx"].a, ref.d["Kxx"].a)
+    assert len(threads) > 1
+    writes = []
+
+    class Rec(FakeFile):
+        def create_dataset(self, *a, **k):
+            ds_ = super().create_dataset(*a, **k)
+            orig = ds_.__class__.__setitem__
+
+            class W(ds_.__class__):
+                def __setitem__(self, key, v):
+                    writes.append((key[1].start, key[2].start))
+                    orig(self, key, v)
+            ds_.__class__ = W
+            return ds_
+
+    def bad(x, x2, same, diag):
+        k = kern(x, x2, same, diag)
+        if x[0, 0, 0, 0] == X[16, 0, 0, 0]:          # the tiles of row block 2
+            k[0, 0] = np.nan
+        return k
+
+    with pytest.raises(FloatingPointError, match="16,16"):
+        save_K(Rec(), bad, "Kxx", ds, None, False, 8, print_interval=1e9, overlap=overlap)
+    order = [(0, 0), (0, 8), (0, 16), (0, 24), (0, 32), (8, 8), (8, 16), (8, 24), (8, 32)]
+    assert writes == order

@@ -380,31 +380,32 @@ def test_mixed_backend_group_string():
     assert "gloo" in got[0][1] and "," in got[0][1]
 
 
-def test_symmetric_rows_and_check_alpha():
-    """rows of the symmetric matrix from its upper triangle only (NaN below), jitter on the
-    diagonal; the check passes scipy's α and rejects a perturbed one"""
+def test_mirror_and_check_alpha():
+    """the system mirrored below the diagonal from its upper triangle only (NaN below);
+    the check passes scipy's α and rejects the α of a factor wrong in one small block of
+    rows (a corrupted trailing-update tile: the residual sits in those rows only)"""
     import scipy.linalg
-    from cnn_gp.solve import (alpha_backward_error, check_alpha, check_rows_index,
-                              symmetric_rows)
+    from cnn_gp.solve import alpha_backward_error, alpha_check_tol, check_alpha, mirror_upper
     rng = np.random.default_rng(1)
-    n = 50
-    G = rng.random((n, 8))
-    A = G @ G.T / 8 + 0.05 * np.eye(n)
+    n = 300
+    G = rng.random((n, 16))
+    A = G @ G.T / 16 + 0.05 * np.eye(n)
     K = A.copy()
     K[np.tril_indices(n, -1)] = np.nan
-    idx = check_rows_index(n, 8)
-    assert len(set(idx)) == 8 and idx == check_rows_index(n, 8) and max(idx) < n
-    rows = symmetric_rows(torch.from_numpy(K), idx, 0.25)
-    want = A[idx] + 0.25 * np.eye(n)[idx]
-    assert np.array_equal(rows.numpy(), want)
-    Y = rng.standard_normal((n, 3))
-    a = scipy.linalg.solve(A + 0.25 * np.eye(n), Y, assume_a="pos")
-    eta = check_alpha(rows, idx, torch.from_numpy(a), torch.from_numpy(Y))
-    assert eta < 1e-15
-    bad = torch.from_numpy(a * (1 + 1e-7 * rng.standard_normal(a.shape)))
-    assert alpha_backward_error(rows, idx, bad, torch.from_numpy(Y)) > 1e-10
+    Kt = torch.from_numpy(K)
+    d = mirror_upper(Kt)
+    assert np.array_equal(Kt.numpy(), A) and np.array_equal(d.numpy(), np.diag(A))
+    Y = torch.from_numpy(rng.standard_normal((n, 3)))
+    a = scipy.linalg.solve(A, Y.numpy(), assume_a="pos")
+    eta = check_alpha(Kt, d, torch.from_numpy(a), Y)
+    assert eta < alpha_check_tol(n) / 100
+    E = np.zeros_like(A)
+    E[200:204, 200:204] = 1e-9 * rng.standard_normal((4, 4))
+    bad = scipy.linalg.solve(A + E + E.T, Y.numpy(), assume_a="pos")
+    r = A @ bad - Y.numpy()
+    assert np.abs(r[:200]).max() < 1e-12 < np.abs(r[200:204]).max()   # a few rows only
+    assert alpha_backward_error(Kt, d, torch.from_numpy(bad), Y) > 10 * alpha_check_tol(n)
+    with pytest.raises(np.linalg.LinAlgError, match="residual check"):
+        check_alpha(Kt, d, torch.from_numpy(bad), Y)
     with pytest.raises(np.linalg.LinAlgError):
-        check_alpha(rows, idx, bad, torch.from_numpy(Y))
-    with pytest.raises(np.linalg.LinAlgError):
-        check_alpha(rows, idx, torch.full_like(bad, float("nan")), torch.from_numpy(Y))
-    assert check_rows_index(3, 8) == [0, 1, 2] and check_rows_index(5, 0) == []
+        check_alpha(Kt, d, torch.full_like(torch.from_numpy(a), float("nan")), Y)
