@@ -31,16 +31,19 @@ def create_h5py_dataset(f, batch_size, name, diag, N, N2):
 
 
 def save_K(f, kern, name, X, X2, diag, batch_size, worker_rank=0, n_workers=1,
-           print_interval=2., overlap=2):
+           print_interval=2., overlap=3):
     """Evaluate this worker's tiles with ``kern(x, x2, same, diag) -> np.ndarray`` and
     write them into dataset ``name`` (created if absent; skipped if it exists).
 
-    ``overlap`` (default 2): up to that many tiles are in flight at once, each kern call
+    ``overlap`` (default 3): up to that many tiles are in flight at once, each kern call
     on a helper thread with a HIP stream of its own (torch's current stream is per
     thread), so one tile's host work — the caller's pageable H2D copies, forward's launch
     calls, the synchronous copy back, the finiteness check and the dataset write — runs
-    while the GPU evaluates another (save_kernel.py:21-24's kern synchronises per tile,
-    which left the GPU idle for 30-43% of a B = 200 build, bench.py ``dropin``).  Tiles
+    while the GPU evaluates another, and small tiles' kernels fill each other's tails
+    (save_kernel.py:21-24's kern synchronises per tile, which left the GPU idle for 30-43%
+    of a B = 200 build, bench.py ``dropin``).  Measured at B = 200 on one MI355X
+    (tools/dropin_overlap_probe.py, profiles/r6/r6c_overlap_*.log): ConvNet GP 0.46 ms per
+    tile serial, 0.32 at overlap 3; mnist_as_tf 0.89 → 0.58-0.66.  Tiles
     are still checked and written in the reference's order, every tile's values are the
     same bits (a tile depends on its own images only), and an exception of a kern call
     or of the finiteness check surfaces in that order.  ``overlap=1`` calls kern on the
