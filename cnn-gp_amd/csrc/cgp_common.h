@@ -328,6 +328,26 @@ __device__ __forceinline__ void horner_q(double (&p)[R], const double (&u)[R], C
 // of the pair's items, netfuse.hip vote_lanes), so a pair's polynomial depends on its own
 // pixels only and a wave whose groups disagree runs each chosen polynomial under its lanes'
 // exec mask
+// The vote's interval test on the high 32 bits of u = x4 (u > 0: floored at 2^-51, or NaN):
+// for positive doubles the high word is monotone in the value, and the thresholds 0.5 / 1 /
+// 1.5 have zero low words, so hi(u) < hi(thr) implies u < thr — conservative (u within
+// 2^-20 relative below a threshold, or equal to it, takes the next longer polynomial,
+// whose interval also holds it); NaN pixels (high word 0x7ff8…) take the longest one.
+// The max over a lane's R pixels is then 32-bit (v_max3_u32: two pixels per instruction)
+// instead of R − 1 v_max_f64.  CGP_RELU_VOTE_HI=0 restores the fp64 max.
+#ifndef CGP_RELU_VOTE_HI
+#define CGP_RELU_VOTE_HI 1
+#endif
+__device__ __forceinline__ unsigned vote_hi(double v) {
+    return (unsigned)(__builtin_bit_cast(unsigned long long, v) >> 32);
+}
+template <int R>
+__device__ __forceinline__ unsigned vote_hi_max(const double (&u)[R]) {
+    unsigned m = vote_hi(u[0]);
+#pragma unroll
+    for (int r = 1; r < R; ++r) m = m > vote_hi(u[r]) ? m : vote_hi(u[r]);
+    return m;
+}
 template <int R, bool QIN, int AD = 0>
 __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
                                          const double (&v2)[R], const PolyTab& tab,
@@ -353,16 +373,25 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         sx[r] = (st[r] * u[r]) * sq4;
     }
     if constexpr (AD == 2) {
+        const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
+        auto all_seg = [&](bool pred) { return (__ballot(pred) & seg) == ex; };
+#if CGP_RELU_VOTE_HI
+        const unsigned hm = vote_hi_max<R>(u);
+        if (all_seg(hm < vote_hi(4.0 * kReluAdaptX0))) {
+            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+        } else if (all_seg(hm < vote_hi(4.0 * kReluAdaptX1))) {
+            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        } else if (all_seg(hm < vote_hi(4.0 * kReluAdaptX2))) {
+#else
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
-        const unsigned long long ex = __builtin_amdgcn_read_exec() & seg;
-        auto all_seg = [&](bool pred) { return (__ballot(pred) & seg) == ex; };
         if (all_seg(um <= 4.0 * kReluAdaptX0)) {
             horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
         } else if (all_seg(um <= 4.0 * kReluAdaptX1)) {
             horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
         } else if (all_seg(um <= 4.0 * kReluAdaptX2)) {
+#endif
             horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
         } else {
             horner_q<R, kReluPolyDegD>(p, u, tab.dq);
@@ -370,6 +399,14 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
     } else if constexpr (AD == 1) {
         // the largest x4 = 4x of the lane's pixels; the wave takes the shortest polynomial
         // whose interval holds every active lane's pixels (x4 <= 4·kReluAdaptX)
+#if CGP_RELU_VOTE_HI
+        const unsigned hm = vote_hi_max<R>(u);
+        if (__all(hm < vote_hi(4.0 * kReluAdaptX0))) {
+            horner_q<R, kReluAdaptDeg0>(p, u, tab.a0);
+        } else if (__all(hm < vote_hi(4.0 * kReluAdaptX1))) {
+            horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
+        } else if (__all(hm < vote_hi(4.0 * kReluAdaptX2))) {
+#else
         double um = u[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) um = __builtin_fmax(um, u[r]);
@@ -378,6 +415,7 @@ __device__ __forceinline__ void relu_q_n(double (&c)[R], const double (&v1q)[R],
         } else if (__all(um <= 4.0 * kReluAdaptX1)) {
             horner_q<R, kReluAdaptDeg1>(p, u, tab.a1);
         } else if (__all(um <= 4.0 * kReluAdaptX2)) {
+#endif
             horner_q<R, kReluAdaptDeg2>(p, u, tab.a2);
         } else {
             horner_q<R, kReluPolyDegD>(p, u, tab.dq);

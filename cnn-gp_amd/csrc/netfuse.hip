@@ -482,14 +482,15 @@ __device__ __forceinline__ unsigned long long vote_lanes(int it) {
     const unsigned long long top = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
     return top & ~((1ull << a) - 1ull);
 }
-template <typename T, bool EX, bool DU, class G>
+// PRE: weight and bias arrive already scaled (a compiled program's records, prog_recs)
+template <typename T, bool EX, bool DU, class G, bool PRE = false>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
                                          const NetP<T>& p, const Pairs& pr) {
     constexpr int NP = G::NP;
     const int tid = opaque_tid();
     const PolyTab tab = poly_table();
     // a conv feeding the fp64 closed-form ReLU produces c/4 (exact: w/4, b/4) for relu_q_n
-    const T qs = kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
+    const T qs = !PRE && kQuarter<T, EX> && op.relu ? T(0.25) : T(1);
     const T w = T(op.weight) * qs, b = T(op.bias) * qs;
     const int arena = NP == 1 ? 0 : p.lds_elems;
     prio_mem<NP, G::HW>();
@@ -928,6 +929,47 @@ __device__ __forceinline__ void net_move(T* __restrict__ lds, const cgp_net_op& 
     }
 }
 
+// The same move for a compiled program (geometry, slot and pitches compile-time): pass k
+// covers elements e = k·kNT + tid of the NP pairs' H×W maps, all passes unrolled.  The
+// launch's state base (u0 − ubeg)·code + add is scalar (u0 is uniform), so an element's
+// global address is that SGPR base plus a 32-bit lane offset q·code + l, and its LDS cell
+// q·arena + r·ws + c comes from compile-time divisions: about 12 VALU per element where
+// the generic loop above spent about 25 (64-bit address math, signed divisions by runtime
+// sizes; ISA count, tools/isa_attrib.py).  CGP_NET_MOVE_C=0 keeps the generic loop.
+#ifndef CGP_NET_MOVE_C
+#define CGP_NET_MOVE_C 1
+#endif
+template <typename T, int KIND, int NP, int H_, int W_, int SLOT, int WS>
+__device__ __forceinline__ void net_move_c(T* __restrict__ lds, const cgp_net_op& op,
+                                           const NetP<T>& p, const Pairs& pr) {
+    const int tid = opaque_tid();
+    constexpr int HW = H_ * W_, N = NP * HW, KP = (N + kNT - 1) / kNT;
+    const int arena = NP == 1 ? 0 : p.lds_elems;
+    const unsigned long long u0 =
+        ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)pr.u0 >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((unsigned)pr.u0);
+    const unsigned code = (unsigned)__builtin_amdgcn_readfirstlane(op.code);
+    const GP<char> base = ubase(op.var_x) +
+                          ((size_t)(u0 - (unsigned long long)p.ubeg) * code + (size_t)op.add) *
+                              sizeof(T);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const int e = k * kNT + tid;
+        if (N % kNT == 0 || e < N) {
+            const unsigned q = NP == 1 ? 0u : (unsigned)udiv(e, HW);
+            const unsigned l = (unsigned)e - q * (unsigned)HW;
+            const unsigned r = (unsigned)udiv((int)l, W_), c = l - r * (unsigned)W_;
+            T* cell = lds + (SLOT + (int)q * arena + (int)(r * (unsigned)WS + c));
+            typedef __attribute__((address_space(1))) T* GW;   // the state record, writable
+            GW g = (GW)(base + (size_t)((q * code + l) * (unsigned)sizeof(T)));
+            if constexpr (KIND == CGP_NET_LOAD)
+                *cell = *g;
+            else
+                *g = *cell;
+        }
+    }
+}
+
 // Zero the halo cells of the slot whose pixel (0, 0) is at `origin` (code = (HL << 8) |
 // gap, see cgp_net_op.zero_halo): HL cells before it and `gap` after each of the h rows.
 // Disjoint from every data cell, so it needs no barrier against the op's own writes.
@@ -1068,6 +1110,12 @@ __device__ __forceinline__ void net_op(T* __restrict__ lds, const cgp_net_op& op
 // net_programs.h).  A program kernel runs its ops as straight-line code: kind, geometry,
 // LDS offsets and strides are immediates, only weight / bias / variance pointers are read
 // from the launch's op records.  The host picks it with cgp_net_program().
+// compiled programs take their convs' ReLU scaling (w/4, b/4) from prog_recs, applied once
+// per workgroup (two VALU ops less per conv and pair); CGP_NET_PRESCALE=0: per op as before
+#ifndef CGP_NET_PRESCALE
+#define CGP_NET_PRESCALE 1
+#endif
+constexpr bool kNetPrescale = CGP_NET_PRESCALE != 0;
 struct ProgOp {
     int kind, code, src, dst, add, ws_in, ws_out, relu, h, w, dst2, zero_halo;
 };
@@ -1148,12 +1196,17 @@ __device__ __forceinline__ void prog_ops(T* __restrict__ lds, const NetP<T>& p, 
             }
         }
         if constexpr (o.kind == CGP_NET_CONV) {
-            net_conv<T, false, DU, typename ProgGeo<PID, K, NP>::G>(lds, op, p, pr);
+            net_conv<T, false, DU, typename ProgGeo<PID, K, NP>::G, kNetPrescale>(lds, op, p,
+                                                                                 pr);
         } else if constexpr (o.kind == CGP_NET_RELU || o.kind == CGP_NET_LINEAR ||
                              o.kind == CGP_NET_MOMENTS) {
             net_elem<T, false, DU, o.kind, o.h, o.w, NP>(lds, op, p, pr);
         } else if constexpr (o.kind == CGP_NET_LOAD || o.kind == CGP_NET_STORE) {
-            net_move<T, o.kind, NP>(lds, op, p, pr);
+            if constexpr (CGP_NET_MOVE_C)
+                net_move_c<T, o.kind, NP, o.h, o.w, o.kind == CGP_NET_LOAD ? o.dst : o.src,
+                           o.kind == CGP_NET_LOAD ? o.ws_out : o.ws_in>(lds, op, p, pr);
+            else
+                net_move<T, o.kind, NP>(lds, op, p, pr);
         }
         lds_barrier();
         prog_ops<T, DU, NP, PID, K + 1>(lds, p, pr, tid, recs);
@@ -1209,7 +1262,13 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
     if constexpr (PID >= 0) {
         for (int k = tid; k < kRecsOf<PID>; k += kNTof<NP>) {
             const cgp_net_op& r = p.ops[k];
-            prog_recs[k] = ProgRec{r.weight, r.bias, r.var_x, r.var_y, r.var2_x, r.var2_y};
+            // a conv feeding the fp64 closed-form ReLU runs on w/4, b/4 (net_conv): scaled
+            // here once per workgroup (exact) instead of per op and pair
+            const ProgOp& o = kProgOps[kProgs[PID < 0 ? 0 : PID].first + k];
+            const double qs =
+                kNetPrescale && kQuarter<T, false> && o.kind == CGP_NET_CONV && o.relu ? 0.25 : 1.0;
+            prog_recs[k] = ProgRec{r.weight * qs, r.bias * qs, r.var_x, r.var_y, r.var2_x,
+                                   r.var2_y};
         }
     }
     lds_barrier();
