@@ -57,9 +57,12 @@ MAX_LDS_BYTES = 160 * 1024
 SMALL_STATE_BYTES = 512 << 20
 # Tile recipes (TileRecipe): a forward's launch sequence kept per (tile shape, stream)
 # while its persistent buffers (variance maps, stage states) take at most RECIPE_MAX_BYTES,
-# at most RECIPE_SLOTS per NetPlan (least recently used dropped first).  0 turns them off.
+# at most RECIPE_SLOTS recipes and RECIPE_TOTAL_BYTES per NetPlan (least recently used
+# dropped first: save_K's helper threads each hold the 4-5 tile shapes of a build on
+# their own stream).  RECIPE_MAX_BYTES = 0 turns them off.
 RECIPE_MAX_BYTES = int(os.environ.get("CGP_RECIPE_MAX_MB", "512")) << 20
-RECIPE_SLOTS = 8
+RECIPE_SLOTS = 32
+RECIPE_TOTAL_BYTES = 4 << 30
 
 
 class Unsupported(Exception):
@@ -860,7 +863,8 @@ class NetPlan:
             if rec is None:
                 return None
             cache[key] = rec
-            while len(cache) > RECIPE_SLOTS:
+            while len(cache) > RECIPE_SLOTS or (
+                    len(cache) > 1 and sum(r.nbytes for r in cache.values()) > RECIPE_TOTAL_BYTES):
                 cache.popitem(last=False)
             return rec
 
@@ -908,6 +912,7 @@ class TileRecipe:
         if vbytes + sbytes > RECIPE_MAX_BYTES:
             return None
         r = cls()
+        r.nbytes = vbytes + sbytes
         r.shape = (n1, n2, tuple(x.shape[1:]), x.dtype, x.device)
         r.same = bool(same)
         r.vbuf = torch.empty((vbytes // item,), dtype=x.dtype, device=x.device)

@@ -43,6 +43,10 @@ def main():
     ap.add_argument("--config", default="mnist_paper_convnet_gp")
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--tile", type=int, default=200)
+    ap.add_argument("--overlaps", default="1,2,3")
+    ap.add_argument("--pins", default="0,1")
+    ap.add_argument("--recipes", default="1,0")
+    ap.add_argument("--reps", type=int, default=1)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = importlib.import_module(f"configs.{args.config}")
@@ -63,12 +67,12 @@ def main():
             ev.append((threading.get_ident(), t0, t1, t2, time.perf_counter()))
             return out
 
-    for pin in (False, True):
+    for pin in [bool(int(v)) for v in args.pins.split(",")]:
         X = X0.pin_memory() if pin else X0
         ds = TensorDataset(X, torch.zeros(args.n, dtype=torch.int64))
-        for recipes in (True, False):
+        for recipes in [bool(int(v)) for v in args.recipes.split(",")]:
             netplan.RECIPE_MAX_BYTES = (512 << 20) if recipes else 0
-            for ov in (1, 2, 3):
+            for ov in [int(v) for v in args.overlaps.split(",") for _ in range(args.reps)]:
                 with contextlib.redirect_stdout(sys.stderr):
                     save_K(MemH5(), kern, "Kxx", ds, None, False, args.tile, overlap=ov,
                            print_interval=1e9)

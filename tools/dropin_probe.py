@@ -100,12 +100,13 @@ def main():
 
     pr = cProfile.Profile()
     with contextlib.redirect_stdout(sys.stderr):
-        pr.enable()
-        save_K(MemH5(), kern, "Kxx", ds, None, False, args.tile, print_interval=1e9)
+        pr.enable()      # serial (overlap 1): the calling thread runs every kern call
+        save_K(MemH5(), kern, "Kxx", ds, None, False, args.tile, print_interval=1e9,
+               overlap=1)
         torch.cuda.synchronize()
         pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(40)
     print(s.getvalue())
 
 
