@@ -85,9 +85,9 @@ SIMDS = 256 * 4                # 256 CUs × 4 SIMDs
 CLOCK_HZ = 2.4e9               # peak engine clock
 # committed PMC passes, newest first (a config missing from a newer file is looked up in
 # the older one)
-PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r5", "r4", "r3")]
+PMC_FILES = [os.path.join(ROOT, "profiles", r, "net_pmc.json") for r in ("r6", "r5", "r4", "r3")]
 # the fp64 flop counters of the same kernel code (tools/pmc_flops.sh)
-FLOPS_FILES = [os.path.join(ROOT, "profiles", r, "flops_pmc.json") for r in ("r5",)]
+FLOPS_FILES = [os.path.join(ROOT, "profiles", r, "flops_pmc.json") for r in ("r6", "r5")]
 CALIB_FILES = [os.path.join(ROOT, "profiles", r, "cpu_calibration.json") for r in ("r4", "r2")]
 DIST_TIMEOUT_S = float(os.environ.get("CGP_DIST_TIMEOUT_S", "120"))
 
