@@ -31,17 +31,18 @@ def create_h5py_dataset(f, batch_size, name, diag, N, N2):
 
 
 def save_K(f, kern, name, X, X2, diag, batch_size, worker_rank=0, n_workers=1,
-           print_interval=2., overlap=3):
+           print_interval=2., overlap=4):
     """Evaluate this worker's tiles with ``kern(x, x2, same, diag) -> np.ndarray`` and
     write them into dataset ``name`` (created if absent; skipped if it exists).
 
-    ``overlap`` (default 3): up to that many tiles are in flight at once, each kern call
+    ``overlap`` (default 4): up to that many tiles are in flight at once, each kern call
     on a helper thread with a HIP stream of its own (torch's current stream is per
     thread), so one tile's host work — the caller's pageable H2D copies, forward's launch
     calls, the synchronous copy back, the finiteness check and the dataset write — runs
     while the GPU evaluates another, and small tiles' kernels fill each other's tails
     (save_kernel.py:21-24's kern synchronises per tile, which left the GPU idle for 30-43%
-    of a B = 200 build, bench.py ``dropin``).  Measured at B = 200 on one MI355X
+    of a B = 200 build, bench.py ``dropin``).  The helper threads persist across save_K
+    calls.  Measured at B = 200 on one MI355X
     (tools/dropin_overlap_probe.py, profiles/r6/r6c_overlap_*.log): ConvNet GP 0.46 ms per
     tile serial, 0.32 at overlap 3; mnist_as_tf 0.89 → 0.58-0.66.  Tiles
     are still checked and written in the reference's order, every tile's values are the
@@ -75,36 +76,61 @@ def save_K(f, kern, name, X, X2, diag, batch_size, worker_rank=0, n_workers=1,
         return
     call = _on_own_stream(kern)
     pending = collections.deque()
-    with ThreadPoolExecutor(max_workers=int(overlap),
-                            thread_name_prefix="cgp-save-K") as pool:
-        try:
-            for same, (i, (x, _y)), (j, (x2, _y2)) in it:
-                pending.append((i, j, x, x2, pool.submit(call, x, x2, same, diag)))
-                if len(pending) >= overlap:
-                    i_, j_, a_, b_, fut = pending.popleft()
-                    write(i_, j_, a_, b_, fut.result())
-            while pending:
+    pool = _pool(int(overlap))
+    try:
+        for same, (i, (x, _y)), (j, (x2, _y2)) in it:
+            pending.append((i, j, x, x2, pool.submit(call, x, x2, same, diag)))
+            if len(pending) >= overlap:
                 i_, j_, a_, b_, fut = pending.popleft()
                 write(i_, j_, a_, b_, fut.result())
-        finally:
-            for *_, fut in pending:        # an error above: nothing more is written
-                fut.cancel()
+        while pending:
+            i_, j_, a_, b_, fut = pending.popleft()
+            write(i_, j_, a_, b_, fut.result())
+    finally:
+        for *_, fut in pending:            # an error above: nothing more is written
+            fut.cancel()
+        for *_, fut in pending:            # and no call is left running behind the caller
+            if not fut.cancelled():
+                try:
+                    fut.result()
+                except Exception:          # noqa: BLE001 - the first error is the one raised
+                    pass
+
+
+# Helper threads live as long as the process (one pool per overlap): a thread keeps its
+# HIP stream, and with it the model's tile recipes (netplan.TileRecipe, one per tile shape
+# and stream), from one save_K to the next — save_kernel.py calls save_K five times.
+_POOLS = {}
+_POOLS_LOCK = threading.Lock()
+_TLS = threading.local()                      # each helper thread's stream per device
+
+
+def _pool(n: int) -> ThreadPoolExecutor:
+    with _POOLS_LOCK:
+        p = _POOLS.get(n)
+        if p is None:
+            p = _POOLS[n] = ThreadPoolExecutor(max_workers=n, thread_name_prefix="cgp-save-K")
+        return p
 
 
 def _on_own_stream(kern):
     """kern wrapped to run under a HIP stream of the calling thread's own (created on the
-    thread's first call) when a GPU is visible; plain kern otherwise."""
+    thread's first call, on the caller's device) when a GPU is visible; plain kern
+    otherwise.  (Handing kern its batches in freshly pinned memory measured slower: the
+    pinned allocations stall the device.)"""
     import torch
     if not torch.cuda.is_available():
         return kern
     dev = torch.cuda.current_device()          # the caller's device, not device 0
-    local = threading.local()
 
     def call(x, x2, same, diag):
-        s = getattr(local, "stream", None)
+        streams = getattr(_TLS, "streams", None)
+        if streams is None:
+            streams = _TLS.streams = {}
+        s = streams.get(dev)
         if s is None:
             torch.cuda.set_device(dev)
-            s = local.stream = torch.cuda.Stream(dev)
+            s = streams[dev] = torch.cuda.Stream(dev)
         with torch.cuda.stream(s):
             k = kern(x, x2, same, diag)
         return k
