@@ -784,8 +784,11 @@ def dropin_leg(cfg_names, n, tiles, dev):
         mk = model_kern(model)
         for B in tiles:
             with contextlib.redirect_stdout(sys.stderr):   # save_K's progress lines
-                # warm: one whole pass (every tile shape, the ragged edge's included)
-                save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9)
+                # warm: two whole passes (every tile shape, the ragged edge's included, on
+                # every helper thread of save_K: each keeps its stream's tile recipes — the
+                # steady state of save_kernel.py's five save_K calls)
+                for _ in range(2):
+                    save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9)
                 torch.cuda.synchronize()
                 f = MemH5()
                 t0 = time.perf_counter()
