@@ -618,3 +618,32 @@ def test_save_K_overlap_writes_the_serial_files(overlap):
         save_K(Rec(), bad, "Kxx", ds, None, False, 8, print_interval=1e9, overlap=overlap)
     order = [(0, 0), (0, 8), (0, 16), (0, 24), (0, 32), (8, 8), (8, 16), (8, 24), (8, 32)]
     assert writes == order
+
+
+def test_save_K_overlap_kern_error_surfaces_in_order():
+    """an exception inside a kern call on a helper thread reaches the caller at that tile's
+    turn; earlier tiles are written, later ones are not"""
+    rng = np.random.default_rng(5)
+    X = torch.from_numpy(rng.random((30, 1, 3, 3)))
+    ds = torch.utils.data.TensorDataset(X, torch.zeros(len(X)))
+    written = []
+
+    class F(FakeFile):
+        def create_dataset(self, *a, **k):
+            d = super().create_dataset(*a, **k)
+
+            class W(d.__class__):
+                def __setitem__(self, key, v):
+                    written.append((key[1].start, key[2].start))
+                    super().__setitem__(key, v)
+            d.__class__ = W
+            return d
+
+    def kern(x, x2, same, diag):
+        if x[0, 0, 0, 0] == X[10, 0, 0, 0] and x2[0, 0, 0, 0] == X[20, 0, 0, 0]:
+            raise ValueError("tile (10, 20) fails")
+        return (x.reshape(len(x), -1) @ x2.reshape(len(x2), -1).T).numpy()
+
+    with pytest.raises(ValueError, match="tile \\(10, 20\\)"):
+        save_K(F(), kern, "Kxx", ds, None, False, 10, print_interval=1e9, overlap=4)
+    assert written == [(0, 0), (0, 10), (0, 20), (10, 10)]
