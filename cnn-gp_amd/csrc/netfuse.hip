@@ -482,6 +482,9 @@ __device__ __forceinline__ unsigned long long vote_lanes(int it) {
     const unsigned long long top = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
     return top & ~((1ull << a) - 1ull);
 }
+#ifndef CGP_NET_RES_UNDEF
+#define CGP_NET_RES_UNDEF 1
+#endif
 // PRE: weight and bias arrive already scaled (a compiled program's records, prog_recs)
 template <typename T, bool EX, bool DU, class G, bool PRE = false>
 __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& op,
@@ -623,6 +626,14 @@ __device__ __forceinline__ void net_conv(T* __restrict__ lds, const cgp_net_op& 
         };
         const bool hazard = hits(op.dst) || (DU && hits(op.dst2));
         T res[G::KV][G::R3];
+#if CGP_NET_RES_UNDEF
+        // an idle item's outputs are never stored: defined by an empty asm, not by 7 zero
+        // moves per item and op
+#pragma unroll
+        for (int kv = 0; kv < G::KV; ++kv)
+#pragma unroll
+            for (int k = 0; k < G::R3; ++k) asm volatile("" : "=v"(res[kv][k]));
+#endif
 #pragma unroll
         for (int kv = 0; kv < G::KV; ++kv) {
             const int it = tid + kv * G::NT;
