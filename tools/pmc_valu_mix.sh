@@ -19,7 +19,7 @@ for v in $VARIANTS; do
     for cfg in $CFGS; do
         tag=${v}_${cfg}
         timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CTR -f csv -d $OUT/$tag -o pmc -- \
-            python3 tools/netbench.py --configs $cfg --reps 1 > $OUT/$tag.log 2>&1
+            python3 tools/netbench.py --configs $cfg --reps 1 ${NB_EXTRA:-} > $OUT/$tag.log 2>&1
         rc=$?
         echo "== $tag rc=$rc"
         if [ $rc -ne 0 ]; then tail -5 $OUT/$tag.log; exit $rc; fi
