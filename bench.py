@@ -62,6 +62,7 @@ import importlib
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import threading
@@ -110,7 +111,7 @@ def parse(argv=None):
                    help="skip the float32 repeat of the Kxx legs")
     p.add_argument("--no-dropin", action="store_true",
                    help="skip the literal save_kernel.py loop (save_K + per-tile kern)")
-    p.add_argument("--dropin-n", type=int, default=2048)
+    p.add_argument("--dropin-n", type=int, default=4096)
     p.add_argument("--no-fullscale", action="store_true")
     p.add_argument("--no-fullscale-f32", action="store_true",
                    help="skip the float32-kernel repeat of the full-scale leg")
@@ -752,13 +753,14 @@ def build_kxx(mk, model, X, K, tiles, B, n):
             view.copy_(model(xi) if same else model(xi, X[j * B:(j + 1) * B], False, False))
 
 
-def dropin_leg(cfg_names, n, tiles, dev):
+def dropin_leg(cfg_names, n, tiles, dev, reps=5):
     """exp_mnist_resnet/save_kernel.py:19-29 verbatim in effect: the float32 model
     (config.initial_model.cuda()), host float32 images in a Dataset, and
     ``kern(x, x2, same, diag) = model(x.cuda(), x2.cuda(), same, diag).cpu().numpy()`` driven
     tile by tile by save_K (kernel_save_tools.py:26-58: ProductIterator batches, the
     isfinite check, the write into a float32 (1, N, N) dataset; an in-memory stand-in for
-    the h5py file).  Beside it, the bound build (the bench's step: maps once, tiles in
+    the h5py file), timed ``reps`` times after two warm passes (the median is reported:
+    one pass is 20-100 ms, and single passes spread by ±15%).  Beside it, the bound build (the bench's step: maps once, tiles in
     place, no host copies) on the same images, model and tile size; the two matrices are
     compared on the upper tiles.  pairs = N(N−1)/2 for both (the headline's count)."""
     import contextlib
@@ -769,16 +771,35 @@ def dropin_leg(cfg_names, n, tiles, dev):
     out = {}
     for name in cfg_names:
         cfg = importlib.import_module(f"configs.{name}")
-        model = cfg.initial_model.to(dev)           # float32 buffers: save_kernel.py:19
+        # float32 buffers, as save_kernel.py:19 gets them from a fresh import (the fp64 legs
+        # before this one converted the shared config module in place)
+        model = cfg.initial_model.to(dev, torch.float32)
         C = getattr(cfg, "in_channels", 1)
         side = 32 if C == 3 else 28
         g = torch.Generator().manual_seed(0)
         X = torch.rand((n, C, side, side), generator=g, dtype=torch.float32)
         ds = TensorDataset(X, torch.zeros(n, dtype=torch.int64))
 
+        trace = []
+        pin = os.environ.get("CGP_DROPIN_PIN", "1") != "0"   # save_K's default: pinned
+
         def kern(x, x2, same, diag):                # save_kernel.py:21-24
             with torch.no_grad():
                 return model(x.cuda(dev), x2.cuda(dev), same, diag).detach().cpu().numpy()
+
+        if os.environ.get("CGP_DROPIN_TRACE"):      # per-call phases (diagnostic only)
+            def kern(x, x2, same, diag):            # noqa: F811
+                with torch.no_grad():
+                    t0 = time.perf_counter()
+                    a, b = x.cuda(dev), x2.cuda(dev)
+                    t1 = time.perf_counter()
+                    k = model(a, b, same, diag)
+                    t2 = time.perf_counter()
+                    o = k.detach().cpu()
+                    t3 = time.perf_counter()
+                    o = o.numpy()
+                    trace.append((t1 - t0, t2 - t1, t3 - t2))
+                    return o
 
         Xd = X.to(dev)
         mk = model_kern(model)
@@ -788,20 +809,27 @@ def dropin_leg(cfg_names, n, tiles, dev):
                 # every helper thread of save_K: each keeps its stream's tile recipes — the
                 # steady state of save_kernel.py's five save_K calls)
                 for _ in range(2):
-                    save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9)
+                    save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9, pin=pin)
                 torch.cuda.synchronize()
-                f = MemH5()
-                t0 = time.perf_counter()
-                save_K(f, kern, "Kxx", ds, None, False, B, print_interval=1e9)
-                el = time.perf_counter() - t0
+                els = []
+                trace.clear()
+                for _ in range(reps):                   # one pass is 20-100 ms: the median
+                    f = MemH5()
+                    t0 = time.perf_counter()
+                    save_K(f, kern, "Kxx", ds, None, False, B, print_interval=1e9, pin=pin)
+                    els.append(time.perf_counter() - t0)
+            el = statistics.median(els)
             K = torch.full((n, n), float("nan"), dtype=torch.float32, device=dev)
             sched = tile_schedule(n, None, B, 0, 1)
             build_kxx(mk, model, Xd, K, sched, B, n)        # warm
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            build_kxx(mk, model, Xd, K, sched, B, n)
-            torch.cuda.synchronize()
-            el_b = time.perf_counter() - t0
+            els_b = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                build_kxx(mk, model, Xd, K, sched, B, n)
+                torch.cuda.synchronize()
+                els_b.append(time.perf_counter() - t0)
+            el_b = statistics.median(els_b)
             Kf, Kb = f.d["Kxx"][0], K.cpu().numpy()
             mask = ~np.isnan(Kf)
             diff = float(np.max(np.abs(Kf[mask] - Kb[mask]) / np.abs(Kb[mask])))
@@ -810,6 +838,9 @@ def dropin_leg(cfg_names, n, tiles, dev):
                 "pairs_per_s": round(pairs / el), "s": round(el, 4), "tiles": len(sched),
                 "ms_per_tile": round(el / len(sched) * 1e3, 3),
                 "bound_pairs_per_s": round(pairs / el_b), "over_bound": round(el_b / el, 3),
+                "reps": reps, "s_range": [round(min(els), 4), round(max(els), 4)],
+                **({"trace_ms_h2d_fwd_d2h": [round(sum(t[c] for t in trace) / len(trace) * 1e3,
+                                                   3) for c in range(3)]} if trace else {}),
                 "max_rel_diff_vs_bound": diff}
         del Xd
         torch.cuda.empty_cache()

@@ -1083,13 +1083,39 @@ def test_save_K_overlap_bit_equal_on_device():
             return self.d[name]
 
     outs = []
-    for ov in (1, 2, 4):
+    for ov, pin in ((1, False), (1, True), (2, True), (4, True), (4, False)):
         f = F()
-        save_K(f, kern, "Kxx", ds, None, False, 16, print_interval=1e9, overlap=ov)
+        save_K(f, kern, "Kxx", ds, None, False, 16, print_interval=1e9, overlap=ov, pin=pin)
         outs.append(f.d["Kxx"])
     assert np.isfinite(outs[0][0][np.triu_indices(70)]).all()
     for o in outs[1:]:
         np.testing.assert_array_equal(o, outs[0])
+    assert not X.is_pinned()                   # the caller's dataset is left as it was
+
+
+def test_save_K_hands_kern_pinned_batches():
+    """pin=True: kern's batches are views of one page-locked copy of the dataset (also
+    under Subset / ConcatDataset); pin=False hands the caller's pageable rows"""
+    from cnn_gp import save_K
+    X = torch.rand((48, 1, 28, 28), generator=torch.Generator().manual_seed(5))  # 3 tiles
+    base = torch.utils.data.TensorDataset(X, torch.zeros(len(X)))
+    seen = []
+
+    def kern(x, x2, same, diag):
+        seen.append((x.is_pinned(), x2.is_pinned()))
+        return np.ones((len(x), len(x2)), np.float32)
+
+    class F(dict):
+        def create_dataset(self, name, shape, dtype, fillvalue, chunks, maxshape):
+            self[name] = np.full(shape, fillvalue, dtype=dtype)
+            return self[name]
+
+    for ds in (base, torch.utils.data.Subset(base, range(5, 37)),
+               torch.utils.data.ConcatDataset([base, base])):
+        for pin in (True, False):
+            seen.clear()
+            save_K(F(), kern, "K", ds, ds, False, 16, print_interval=1e9, overlap=2, pin=pin)
+            assert seen and all(a == pin and b == pin for a, b in seen), (type(ds), pin)
 
 
 @pytest.mark.parametrize("n,nrhs", [(1, 1), (63, 10), (64, 3), (65, 17), (200, 10),

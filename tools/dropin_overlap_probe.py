@@ -8,6 +8,7 @@ much of one thread's H2D / launch work ran while another thread waited on the GP
 """
 import argparse
 import contextlib
+import gc
 import importlib
 import os
 import sys
@@ -42,15 +43,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="mnist_paper_convnet_gp")
     ap.add_argument("--n", type=int, default=2048)
-    ap.add_argument("--tile", type=int, default=200)
+    ap.add_argument("--tile", default="200", help="tile sizes, run in turn (e.g. 200,1024)")
     ap.add_argument("--overlaps", default="1,2,3")
     ap.add_argument("--pins", default="0,1")
     ap.add_argument("--recipes", default="1,0")
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--gc", default="1", help="1: Python's collector on (default), 0: off, "
+                    "0,1: both, around the timed save_K")
+    ap.add_argument("--model-f64", action="store_true",
+                    help="float64 weight buffers with the float32 images")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = importlib.import_module(f"configs.{args.config}")
-    model = cfg.initial_model.to(dev)
+    model = cfg.initial_model.to(dev, torch.float64 if args.model_f64 else torch.float32)
     C = getattr(cfg, "in_channels", 1)
     side = 32 if C == 3 else 28
     X0 = torch.rand((args.n, C, side, side), generator=torch.Generator().manual_seed(0))
@@ -68,24 +73,29 @@ def main():
             return out
 
     for pin in [bool(int(v)) for v in args.pins.split(",")]:
-        X = X0.pin_memory() if pin else X0
+        X = X0                              # save_K(pin=...) pins its own copy
         ds = TensorDataset(X, torch.zeros(args.n, dtype=torch.int64))
         for recipes in [bool(int(v)) for v in args.recipes.split(",")]:
             netplan.RECIPE_MAX_BYTES = (512 << 20) if recipes else 0
-            for ov in [int(v) for v in args.overlaps.split(",") for _ in range(args.reps)]:
+            for tile, ov, gco in [(int(b), int(v), int(g)) for b in args.tile.split(",")
+                                  for v in args.overlaps.split(",")
+                                  for g in args.gc.split(",") for _ in range(args.reps)]:
                 with contextlib.redirect_stdout(sys.stderr):
-                    save_K(MemH5(), kern, "Kxx", ds, None, False, args.tile, overlap=ov,
-                           print_interval=1e9)
+                    save_K(MemH5(), kern, "Kxx", ds, None, False, tile, overlap=ov,
+                           print_interval=1e9, pin=pin)
                     torch.cuda.synchronize()
                     ev.clear()
+                    if not gco:
+                        gc.disable()
                     t = time.perf_counter()
-                    save_K(MemH5(), kern, "Kxx", ds, None, False, args.tile, overlap=ov,
-                           print_interval=1e9)
+                    save_K(MemH5(), kern, "Kxx", ds, None, False, tile, overlap=ov,
+                           print_interval=1e9, pin=pin)
                     el = time.perf_counter() - t
+                    gc.enable()
                 n = len(ev)
                 h2d = sum(e[2] - e[1] for e in ev) / n * 1e3
                 launch = sum(e[3] - e[2] for e in ev) / n * 1e3
-                print(f"pin={int(pin)} recipes={int(recipes)} overlap={ov}: "
+                print(f"B={tile} pin={int(pin)} recipes={int(recipes)} gc={gco} overlap={ov}: "
                       f"{el / n * 1e3:.3f} ms/tile ({args.n * (args.n - 1) / 2 / el / 1e6:.1f} "
                       f"M pairs/s); per call h2d {h2d:.3f} "
                       f"launch {launch:.3f} wait {sum(e[4] - e[3] for e in ev) / n * 1e3:.3f} "
