@@ -1015,23 +1015,6 @@ __device__ __forceinline__ void tri_decode(unsigned s, unsigned nb, unsigned& bi
     bj = (unsigned)(r + ((long long)s - off(r)));
 }
 
-// a wave's last supertile decode: a workgroup walks a supertile's 64 units in order (2 per
-// step in the two-pair head), so the triangular decode — an fp64 square root and its
-// fix-ups, ≈ 45 VALU, which every wave of the head ran for both units of every step — is
-// redone only when the supertile changes.  The unit index is uniform (an LDS broadcast), so
-// the cached block is scalar (SGPRs); CGP_NET_UNIT_CACHE=0 decodes every unit.
-#ifndef CGP_NET_UNIT_CACHE
-#define CGP_NET_UNIT_CACHE 1
-#endif
-struct UnitCache {
-    unsigned s = ~0u, bi = 0, bj = 0;
-};
-__device__ __forceinline__ long long uniform64(long long v) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-
 // tile unit u (supertile, pair within it) -> (i, j); false if outside the tile
 template <typename T>
 __device__ __forceinline__ bool unit_pair(const NetP<T>& p, long long u, unsigned& i,
@@ -1046,28 +1029,6 @@ __device__ __forceinline__ bool unit_pair(const NetP<T>& p, long long u, unsigne
     }
     i = bi * kST + (q >> kSTL);
     j = bj * kST + (q & (kST - 1u));
-    return u < p.units && i < p.n1 && j < p.n2;
-}
-// the same for a uniform u, through the wave's supertile cache
-template <typename T>
-__device__ __forceinline__ bool unit_pair_c(const NetP<T>& p, long long u, unsigned& i,
-                                            unsigned& j, UnitCache& c) {
-    if constexpr (!CGP_NET_UNIT_CACHE) return unit_pair(p, u, i, j);
-    const unsigned s = (unsigned)(u >> (2 * kSTL)), q = (unsigned)u & (kST * kST - 1u);
-    if (s != c.s) {                       // uniform branch: once per supertile
-        unsigned bi, bj;
-        if (p.same) {
-            tri_decode(s, p.nbi, bi, bj);
-        } else {
-            bi = s / p.nbj;
-            bj = s - bi * p.nbj;
-        }
-        c.s = s;
-        c.bi = __builtin_amdgcn_readfirstlane(bi);
-        c.bj = __builtin_amdgcn_readfirstlane(bj);
-    }
-    i = c.bi * kST + (q >> kSTL);
-    j = c.bj * kST + (q & (kST - 1u));
     return u < p.units && i < p.n1 && j < p.n2;
 }
 
@@ -1347,10 +1308,8 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
         adv ^= 1;
         return v;
     };
-    UnitCache ucache;
     for (long long u = advance(); u < end; u = advance()) {
         if (tid == 0) grab = atomicAdd(ctr, 1ull);
-        u = uniform64(u);
         Pairs pr;
         pr.tab = pair_tab;
         pr.u0 = u;
@@ -1368,7 +1327,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
 #pragma unroll
             for (int s = 0; s < UN; ++s) {
                 unsigned is = 0, js = 0;
-                const bool vs = u + s < end && unit_pair_c(p, u + s, is, js, ucache);
+                const bool vs = u + s < end && unit_pair(p, u + s, is, js);
                 const bool ws = vs && !(p.same && js <= is);
                 any |= ws;
                 if (s == q) {
@@ -1412,7 +1371,7 @@ __global__ __launch_bounds__(kNTof<NP>) __attribute__((amdgpu_waves_per_eu(WPE))
             }
         } else {
             if constexpr (NP == 1) {
-                if (!unit_pair_c(p, u, pr.i, pr.j, ucache)) continue;
+                if (!unit_pair(p, u, pr.i, pr.j)) continue;
                 pr.i = __builtin_amdgcn_readfirstlane(pr.i);   // uniform: scalar map offsets
                 pr.j = __builtin_amdgcn_readfirstlane(pr.j);
                 if (p.same && pr.j <= pr.i) {
