@@ -759,16 +759,22 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
     ``kern(x, x2, same, diag) = model(x.cuda(), x2.cuda(), same, diag).cpu().numpy()`` driven
     tile by tile by save_K (kernel_save_tools.py:26-58: ProductIterator batches, the
     isfinite check, the write into a float32 (1, N, N) dataset; an in-memory stand-in for
-    the h5py file), timed ``reps`` times after two warm passes (the median is reported:
-    one pass is 20-100 ms, and single passes spread by ±15%).  Beside it, the bound build (the bench's step: maps once, tiles in
-    place, no host copies) on the same images, model and tile size; the two matrices are
-    compared on the upper tiles.  pairs = N(N−1)/2 for both (the headline's count)."""
+    the h5py file), timed ``reps`` times after two warm passes (the median is reported: one
+    pass is 20-140 ms, and single passes spread by ±15%).  Beside it, the bound build (the
+    bench's step: maps once, tiles in place, no host copies) on the same images, model and
+    tile size.  The two matrices are compared on the upper tiles after every case has been
+    timed: the comparison's 64 MB pageable copy back made the helper threads' next-case
+    H2D copies wait on the other threads' kernels (ConvNet B = 1024: 0.38 → 4-7 ms per
+    call, profiles/r6/r6x_dropin_copy_stall.log).  pairs = N(N−1)/2 for both (the
+    headline's count).  CGP_DROPIN_TRACE=1 adds each call's mean H2D / forward / copy-back
+    times (a diagnostic: the timed kern is the plain one otherwise)."""
     import contextlib
     import numpy as np
     from torch.utils.data import TensorDataset
     from cnn_gp.kernel_save_tools import save_K
     pairs = n * (n - 1) // 2
-    out = {}
+    out, checks = {}, []
+    pin = os.environ.get("CGP_DROPIN_PIN", "1") != "0"       # save_K's default: pinned
     for name in cfg_names:
         cfg = importlib.import_module(f"configs.{name}")
         # float32 buffers, as save_kernel.py:19 gets them from a fresh import (the fp64 legs
@@ -779,15 +785,13 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
         g = torch.Generator().manual_seed(0)
         X = torch.rand((n, C, side, side), generator=g, dtype=torch.float32)
         ds = TensorDataset(X, torch.zeros(n, dtype=torch.int64))
-
         trace = []
-        pin = os.environ.get("CGP_DROPIN_PIN", "1") != "0"   # save_K's default: pinned
 
         def kern(x, x2, same, diag):                # save_kernel.py:21-24
             with torch.no_grad():
                 return model(x.cuda(dev), x2.cuda(dev), same, diag).detach().cpu().numpy()
 
-        if os.environ.get("CGP_DROPIN_TRACE"):      # per-call phases (diagnostic only)
+        if os.environ.get("CGP_DROPIN_TRACE"):
             def kern(x, x2, same, diag):            # noqa: F811
                 with torch.no_grad():
                     t0 = time.perf_counter()
@@ -795,10 +799,8 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
                     t1 = time.perf_counter()
                     k = model(a, b, same, diag)
                     t2 = time.perf_counter()
-                    o = k.detach().cpu()
-                    t3 = time.perf_counter()
-                    o = o.numpy()
-                    trace.append((t1 - t0, t2 - t1, t3 - t2))
+                    o = k.detach().cpu().numpy()
+                    trace.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
                     return o
 
         Xd = X.to(dev)
@@ -809,11 +811,12 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
                 # every helper thread of save_K: each keeps its stream's tile recipes — the
                 # steady state of save_kernel.py's five save_K calls)
                 for _ in range(2):
-                    save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9, pin=pin)
+                    save_K(MemH5(), kern, "Kxx", ds, None, False, B, print_interval=1e9,
+                           pin=pin)
                 torch.cuda.synchronize()
                 els = []
                 trace.clear()
-                for _ in range(reps):                   # one pass is 20-100 ms: the median
+                for _ in range(reps):
                     f = MemH5()
                     t0 = time.perf_counter()
                     save_K(f, kern, "Kxx", ds, None, False, B, print_interval=1e9, pin=pin)
@@ -830,20 +833,24 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
                 torch.cuda.synchronize()
                 els_b.append(time.perf_counter() - t0)
             el_b = statistics.median(els_b)
-            Kf, Kb = f.d["Kxx"][0], K.cpu().numpy()
-            mask = ~np.isnan(Kf)
-            diff = float(np.max(np.abs(Kf[mask] - Kb[mask]) / np.abs(Kb[mask])))
-            del K
-            out[f"{name}/B{B}"] = {
+            key = f"{name}/B{B}"
+            checks.append((key, f.d["Kxx"][0], K))
+            out[key] = {
                 "pairs_per_s": round(pairs / el), "s": round(el, 4), "tiles": len(sched),
                 "ms_per_tile": round(el / len(sched) * 1e3, 3),
                 "bound_pairs_per_s": round(pairs / el_b), "over_bound": round(el_b / el, 3),
-                "reps": reps, "s_range": [round(min(els), 4), round(max(els), 4)],
-                **({"trace_ms_h2d_fwd_d2h": [round(sum(t[c] for t in trace) / len(trace) * 1e3,
-                                                   3) for c in range(3)]} if trace else {}),
-                "max_rel_diff_vs_bound": diff}
+                "reps": reps, "s_range": [round(min(els), 4), round(max(els), 4)]}
+            if trace:
+                out[key]["trace_ms_h2d_fwd_d2h"] = [
+                    round(sum(t[c] for t in trace) / len(trace) * 1e3, 3) for c in range(3)]
         del Xd
-        torch.cuda.empty_cache()
+    for key, Kf, K in checks:                       # after every case's timing (docstring)
+        Kb = K.cpu().numpy()
+        mask = ~np.isnan(Kf)
+        out[key]["max_rel_diff_vs_bound"] = float(
+            np.max(np.abs(Kf[mask] - Kb[mask]) / np.abs(Kb[mask])))
+    del checks, K
+    torch.cuda.empty_cache()
     return {"n": n, "dtype": "f32", "cases": out}
 
 
