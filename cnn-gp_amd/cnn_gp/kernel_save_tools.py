@@ -162,7 +162,10 @@ def _pinned(ds):
         ts = ds.tensors
         if not all(t.device.type == "cpu" for t in ts) or all(t.is_pinned() for t in ts):
             return ds
-        return TensorDataset(*(t if t.is_pinned() else t.pin_memory() for t in ts))
+        try:
+            return TensorDataset(*(t if t.is_pinned() else t.pin_memory() for t in ts))
+        except RuntimeError:          # no page-locked memory to spare: the pageable rows
+            return ds
     if kind is Subset:
         inner = _pinned(ds.dataset)
         return ds if inner is ds.dataset else Subset(inner, ds.indices)
