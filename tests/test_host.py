@@ -647,3 +647,16 @@ def test_save_K_overlap_kern_error_surfaces_in_order():
     with pytest.raises(ValueError, match="tile \\(10, 20\\)"):
         save_K(F(), kern, "Kxx", ds, None, False, 10, print_interval=1e9, overlap=4)
     assert written == [(0, 0), (0, 10), (0, 20), (10, 10)]
+
+
+def test_save_K_pin_leaves_datasets_alone_without_a_gpu():
+    """save_K(pin=True) on a host without a GPU: every dataset kind is handed on as it is
+    (the page-locked copy is only made when a device will read the batches)"""
+    from torch.utils.data import ConcatDataset, Subset, TensorDataset
+    from cnn_gp.kernel_save_tools import _pinned
+    X = torch.rand((6, 1, 4, 4))
+    base = TensorDataset(X, torch.zeros(6))
+    for ds in (base, Subset(base, range(1, 5)), ConcatDataset([base, base]), [X[i] for i in range(6)]):
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible")
+        assert _pinned(ds) is ds
