@@ -849,7 +849,8 @@ def dropin_leg(cfg_names, n, tiles, dev, reps=5):
         mask = ~np.isnan(Kf)
         out[key]["max_rel_diff_vs_bound"] = float(
             np.max(np.abs(Kf[mask] - Kb[mask]) / np.abs(Kb[mask])))
-    del checks, K
+    checks.clear()                                  # the matrices go before the next leg
+    K = None
     torch.cuda.empty_cache()
     return {"n": n, "dtype": "f32", "cases": out}
 
